@@ -1,0 +1,185 @@
+/*
+ * wsg_capi.h — C-ABI boundary of the MI355X WebSocket frame codec.
+ *
+ * This is the drop-in boundary for CppServer's per-byte WebSocket hot path
+ * (reference: chronoxor/CppServer 1.0.5.0, class CppServer::WS::WebSocket,
+ * include/server/ws/ws.h:29, source/server/ws/ws.cpp:212-498).
+ *
+ * Plain C types only: pointers, sizes, fixed-layout structs.  No C++ types and
+ * no torch types cross this boundary; no C++ exception ever leaves it.  Every
+ * entry point returns an int status (WSG_OK = 0, negative on failure).
+ *
+ * Device ("d_") buffers are caller-owned and must already be resident in HBM.
+ * Batch entry points are asynchronous on the given HIP stream (pass NULL for
+ * the context's own stream); the caller synchronizes (wsg_sync) before reading
+ * outputs.  Data-dependent errors (a frame that overruns the wire, overlapping
+ * frames) are latched in the context and reported by wsg_sync.
+ *
+ * Thread-safety: one wsg_ctx per host thread.  A ctx is not thread-safe.
+ */
+#ifndef WSG_CAPI_H
+#define WSG_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WSG_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define WSG_OK          0
+#define WSG_EINVAL    (-22)  /* bad argument: NULL pointer, misaligned buffer, overlapping frames */
+#define WSG_ETRUNC    (-61)  /* a frame header/payload runs past the end of the wire */
+#define WSG_ENOMEM    (-12)  /* device or pinned allocation failed / output capacity too small */
+#define WSG_EHIP      (-5)   /* HIP runtime error (no device, launch failure, ...) */
+
+/* ---- opcode byte values (reference ws.h:33-43) ------------------------- */
+#define WSG_FIN    0x80
+#define WSG_TEXT   0x01
+#define WSG_BINARY 0x02
+#define WSG_CLOSE  0x08
+#define WSG_PING   0x09
+#define WSG_PONG   0x0A
+
+/* Required alignment of wire/output device buffers in the batch decode/encode
+ * entry points (hipMalloc and torch allocations satisfy it). */
+#define WSG_ALIGN 16
+
+/* One frame to encode (a batched PrepareSendFrame call, ws.cpp:212).
+ * key is _ws_send_mask[0..3] read as a little-endian uint32, i.e.
+ * byte j of the key is (key >> 8*j) & 0xFF (ws.cpp:244-247, :270). */
+typedef struct wsg_send_desc {
+    uint64_t src_off;   /* payload offset inside d_payload                    */
+    uint64_t len;       /* payload length in bytes (excluding close status)   */
+    uint32_t key;       /* per-connection send mask (ws.cpp:97 / :206)       */
+    int32_t  status;    /* close status, ws.cpp:215 (0 = none)                */
+    uint8_t  opcode;    /* whole first header byte, e.g. WSG_FIN|WSG_BINARY   */
+    uint8_t  mask;      /* nonzero: set MASK bit and emit the 4 key bytes     */
+    uint8_t  _pad[6];
+} wsg_send_desc;        /* 32 bytes */
+
+/* One decoded frame (the per-frame arithmetic of PrepareReceiveFrame,
+ * ws.cpp:320-386). */
+typedef struct wsg_recv_info {
+    uint64_t payload_off; /* absolute offset of the payload in wire and output */
+    uint64_t len;         /* payload length                                    */
+    uint32_t key;         /* receive mask (little-endian), 0 if unmasked       */
+    uint8_t  opcode;      /* b0 & 0x0F (raw; 0 = continuation, ws.cpp:320)     */
+    uint8_t  fin;         /* b0 >> 7 (ws.cpp:321)                              */
+    uint8_t  masked;      /* b1 >> 7 (ws.cpp:322)                              */
+    uint8_t  hdr_len;     /* 2/4/10 (+4 when masked), ws.cpp:331/349/367       */
+    uint8_t  b0;          /* raw first header byte (RSV bits kept)             */
+    int8_t   error;       /* 0, or WSG_ETRUNC / WSG_EINVAL for this frame      */
+    uint8_t  _pad[6];
+} wsg_recv_info;        /* 32 bytes */
+
+typedef struct wsg_ctx wsg_ctx;
+
+/* ---- context ------------------------------------------------------------ */
+/* Bind to HIP device `device`, create a non-blocking stream, small scratch.   */
+int wsg_create(int device, wsg_ctx** out);
+int wsg_destroy(wsg_ctx* ctx);
+/* Synchronize the ctx's stream (or `stream` if non-NULL) and return the first
+ * data-dependent error latched since the last wsg_sync (then clear it).      */
+int wsg_sync(wsg_ctx* ctx, void* stream);
+/* HIP stream owned by the context (a hipStream_t). */
+void* wsg_stream(wsg_ctx* ctx);
+int wsg_abi_version(void);
+/* Human-readable name of a status code. */
+const char* wsg_strerror(int code);
+
+/* ---- batch decode: unmask (PrepareReceiveFrame over many frames) -------- */
+/* d_wire: `wire_len` bytes of concatenated frames.  d_frame_start[i]: wire
+ * offset of frame i (strictly increasing, frames must not overlap; the host
+ * framer produces it with RequiredReceiveFrameSize semantics, ws.cpp:458).
+ * d_out: wire_len bytes; on return it is the wire with every frame's payload
+ * unmasked in place (ws.cpp:399-406); header and gap bytes are copied
+ * unchanged.  d_out may equal d_wire (in-place).  d_info[i] describes frame i
+ * (payload at d_out + d_info[i].payload_off).  d_wire/d_out 16-byte aligned. */
+int wsg_decode_batch(wsg_ctx* ctx, const uint8_t* d_wire, uint64_t wire_len,
+                     const uint64_t* d_frame_start, uint32_t n,
+                     uint8_t* d_out, wsg_recv_info* d_info, void* stream);
+
+/* ---- batch encode: header pack + mask (PrepareSendFrame over many frames) */
+/* Frames are written back to back into d_wire (16-byte aligned, capacity
+ * wire_cap bytes).  d_wire_off[0..n] receives each frame's offset;
+ * d_wire_off[n] is the total wire length.  Byte-exact with ws.cpp:212-271,
+ * including the close-status prefix on CLOSE/PING/PONG opcodes (ws.cpp:215)
+ * and the XOR applied even when mask == 0 (ws.cpp:269-270).                  */
+int wsg_encode_batch(wsg_ctx* ctx, const uint8_t* d_payload,
+                     const wsg_send_desc* d_desc, uint32_t n,
+                     uint8_t* d_wire, uint64_t wire_cap,
+                     uint64_t* d_wire_off, void* stream);
+
+/* ---- fan-out: one payload, k client keys (k x client-style SendBinary) -- */
+/* Frame j = PrepareSendFrame(opcode, mask, payload, len) with
+ * _ws_send_mask = d_keys[j]; frames back to back in d_wire, each
+ * wsg_frame_size(opcode, mask, len, 0) bytes.  d_wire 16-byte aligned.        */
+int wsg_fanout_encode(wsg_ctx* ctx, const uint8_t* d_payload, uint64_t len,
+                      const uint32_t* d_keys, uint32_t k, uint8_t opcode,
+                      int mask, uint8_t* d_wire, uint64_t wire_cap, void* stream);
+
+/* ---- host-staged entry points (host buffers; PCIe in the path) ---------- */
+/* XOR `len` bytes of host `src` into host `dst` with key byte (phase+i)%4 on
+ * the GPU (H2D, kernel, D2H), synchronous.  src may equal dst.               */
+int wsg_xor_host(wsg_ctx* ctx, const void* src, void* dst, size_t len,
+                 uint32_t key, uint32_t phase);
+/* Batch decode of a host wire buffer through pinned staging with copy/compute
+ * overlap.  Same semantics as wsg_decode_batch, host pointers.                */
+int wsg_decode_batch_host(wsg_ctx* ctx, const uint8_t* wire, uint64_t wire_len,
+                          const uint64_t* frame_start, uint32_t n,
+                          uint8_t* out, wsg_recv_info* info);
+
+/* ---- single-frame header helpers (host; same code the kernels run) ------ */
+/* Total frame size PrepareSendFrame produces (ws.cpp:215-252).               */
+uint64_t wsg_frame_size(uint8_t opcode, int mask, uint64_t len, int32_t status);
+/* Write the header (ws.cpp:222-248) into out[0..14); returns its length.     */
+int wsg_header_pack(uint8_t opcode, int mask, uint64_t len, int32_t status,
+                    uint32_t key, uint8_t* out);
+/* Parse a complete header at buf[0..avail) (ws.cpp:320-386).  Returns WSG_OK,
+ * or WSG_ETRUNC when avail is too short for the header.                       */
+int wsg_header_unpack(const uint8_t* buf, uint64_t avail, wsg_recv_info* info);
+
+/* ---- per-connection session (the WebSocket mix-in, ws.h:29) ------------- */
+/* A session is the reference's per-connection codec state; its payload
+ * mask/unmask runs on the GPU through the owning ctx.                         */
+typedef struct wsg_session wsg_session;
+/* Receive callback: kind is WSG_CB_* ; status is the close status.           */
+#define WSG_CB_RECEIVED 1   /* onWSReceived (ws.cpp:445-450) */
+#define WSG_CB_CLOSE    2   /* onWSClose    (ws.cpp:429-443) */
+#define WSG_CB_PING     3   /* onWSPing     (ws.cpp:417-421) */
+#define WSG_CB_PONG     4   /* onWSPong     (ws.cpp:423-427) */
+typedef void (*wsg_receive_cb)(void* user, int kind, const uint8_t* data,
+                               size_t size, int status);
+int wsg_session_create(wsg_ctx* ctx, wsg_session** out);
+int wsg_session_destroy(wsg_session* s);
+/* _ws_send_mask as little-endian uint32 (ws.cpp:97 client / :206 server).   */
+int wsg_session_set_send_key(wsg_session* s, uint32_t key);
+/* PrepareSendFrame (ws.cpp:212): frame copied to out[0..*out_len).           */
+int wsg_session_prepare_send(wsg_session* s, uint8_t opcode, int mask,
+                             const void* buf, size_t size, int32_t status,
+                             uint8_t* out, size_t out_cap, size_t* out_len);
+/* PrepareReceiveFrame (ws.cpp:273): callbacks fire synchronously.            */
+int wsg_session_prepare_receive(wsg_session* s, const void* buf, size_t size,
+                                wsg_receive_cb cb, void* user);
+/* RequiredReceiveFrameSize (ws.cpp:458).                                      */
+size_t wsg_session_required(wsg_session* s);
+/* ClearWSBuffers (ws.cpp:484).                                                */
+int wsg_session_clear(wsg_session* s);
+
+/* ---- kernel timing (measurement hook used by bench.py) ------------------ */
+/* When enabled, the ctx records HIP events around the dominant payload kernel
+ * of every batch call on the stream it is launched on.                        */
+int wsg_timing_enable(wsg_ctx* ctx, int on);
+/* Sum of the dominant-kernel durations (ms) and launch count since the last
+ * reset; synchronizes outstanding events.                                     */
+int wsg_timing_read(wsg_ctx* ctx, double* total_ms, uint64_t* launches, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WSG_CAPI_H */
