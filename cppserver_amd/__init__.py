@@ -1,0 +1,227 @@
+"""cppserver_amd — MI355X-native WebSocket frame codec (CppServer's WS hot path).
+
+The product is the C-ABI library ``_build/libwsg.so`` (include/wsg_capi.h):
+gfx950 HIP kernels for batched header pack/unpack and payload mask/unmask.
+This module is a thin ctypes binding over that ABI for Python callers and the
+test-suite; torch is used only to own device memory and streams.
+
+There is no CPU fallback: if the library or a GPU is missing, ``Codec``
+raises instead of computing anything.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .layout import (  # noqa: F401  (re-exported)
+    CB_CLOSE, CB_PING, CB_PONG, CB_RECEIVED, RECV_INFO, SEND_DESC, WS_BINARY, WS_CLOSE, WS_FIN, WS_PING,
+    WS_PONG, WS_TEXT, WSG_EHIP, WSG_EINVAL, WSG_ENOMEM, WSG_ETRUNC, WSG_OK, frame_size, key_from_bytes,
+)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libwsg.so")
+ROOT = os.path.dirname(_HERE)
+HEADERS = [os.path.join(ROOT, "include", "wsg_capi.h")]
+
+_lib = None
+
+
+class WSGError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        msg = lib().wsg_strerror(code).decode() if _lib is not None else str(code)
+        super().__init__("%s failed: %s (%d)" % (what or "wsg", msg, code))
+
+
+def lib():
+    """Load the HIP codec library; raise loudly if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "cppserver_amd: native library %s is missing; run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(or `make -C cppserver_amd`). There is no CPU fallback." % LIB_PATH
+        )
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i32, sz, ci = (ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32,
+                                 ctypes.c_size_t, ctypes.c_int)
+    sig = {
+        "wsg_abi_version": (ci, []),
+        "wsg_strerror": (ctypes.c_char_p, [ci]),
+        "wsg_create": (ci, [ci, ctypes.POINTER(vp)]),
+        "wsg_destroy": (ci, [vp]),
+        "wsg_sync": (ci, [vp, vp]),
+        "wsg_stream": (vp, [vp]),
+        "wsg_decode_batch": (ci, [vp, vp, u64, vp, u32, vp, vp, vp]),
+        "wsg_encode_batch": (ci, [vp, vp, vp, u32, vp, u64, vp, vp]),
+        "wsg_fanout_encode": (ci, [vp, vp, u64, vp, u32, ctypes.c_uint8, ci, vp, u64, vp]),
+        "wsg_xor_host": (ci, [vp, vp, vp, sz, u32, u32]),
+        "wsg_decode_batch_host": (ci, [vp, vp, u64, vp, u32, vp, vp]),
+        "wsg_frame_size": (u64, [ctypes.c_uint8, ci, u64, i32]),
+        "wsg_header_pack": (ci, [ctypes.c_uint8, ci, u64, i32, u32, vp]),
+        "wsg_header_unpack": (ci, [vp, u64, vp]),
+        "wsg_timing_enable": (ci, [vp, ci]),
+        "wsg_timing_read": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ci]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _np_ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise WSGError(rc, what)
+
+
+# ---- host helpers (pure host functions of the ABI; no device needed) ------
+def header_pack(opcode, mask, length, status=0, key=0):
+    buf = (ctypes.c_uint8 * 16)()
+    n = lib().wsg_header_pack(opcode, 1 if mask else 0, length, status, key, buf)
+    if n < 0:
+        raise WSGError(n, "wsg_header_pack")
+    return bytes(buf[:n])
+
+
+def header_unpack(data):
+    data = bytes(data)
+    info = np.zeros(1, dtype=RECV_INFO)
+    rc = lib().wsg_header_unpack(data, len(data), _np_ptr(info))
+    return rc, info[0]
+
+
+def abi_frame_size(opcode, mask, length, status=0):
+    return int(lib().wsg_frame_size(opcode, 1 if mask else 0, length, status))
+
+
+class Codec:
+    """A wsg_ctx bound to one HIP device.
+
+    Batch methods take torch CUDA (HIP) tensors resident in HBM and run
+    asynchronously on ``stream`` (default: torch's current stream); call
+    :meth:`sync` before reading results on the host.
+    """
+
+    def __init__(self, device=0):
+        import torch
+
+        self._torch = torch
+        if not torch.cuda.is_available():
+            raise WSGError(WSG_EHIP, "Codec: no HIP device visible")
+        self.device = torch.device("cuda", device)
+        self._L = lib()
+        ctx = ctypes.c_void_p()
+        _check(self._L.wsg_create(device, ctypes.byref(ctx)), "wsg_create")
+        self._ctx = ctx
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._L.wsg_destroy(self._ctx)
+            self._ctx = None
+
+    __del__ = close
+
+    # -- streams / sync ----------------------------------------------------
+    def _stream(self, stream):
+        if stream is None:
+            stream = self._torch.cuda.current_stream(self.device)
+        return ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream))
+
+    def sync(self, stream=None):
+        """Synchronize and raise WSGError on a latched data-dependent error."""
+        _check(self._L.wsg_sync(self._ctx, self._stream(stream)), "wsg_sync")
+
+    def sync_status(self, stream=None):
+        return self._L.wsg_sync(self._ctx, self._stream(stream))
+
+    # -- batch decode (unmask) ----------------------------------------------
+    def decode_batch(self, wire, frame_start, out=None, info=None, stream=None):
+        """Unmask every frame of ``wire`` (uint8 CUDA tensor) whose starts are
+        ``frame_start`` (int64 CUDA tensor).  Returns (out, info_bytes)."""
+        t = self._torch
+        n = int(frame_start.numel())
+        if out is None:
+            out = t.empty_like(wire)
+        if info is None:
+            info = t.empty(max(n, 1) * RECV_INFO.itemsize, dtype=t.uint8, device=wire.device)
+        rc = self._L.wsg_decode_batch(self._ctx, ctypes.c_void_p(wire.data_ptr()), wire.numel(),
+                                      ctypes.c_void_p(frame_start.data_ptr()), n,
+                                      ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(info.data_ptr()),
+                                      self._stream(stream))
+        _check(rc, "wsg_decode_batch")
+        return out, info
+
+    # -- batch encode (mask) --------------------------------------------------
+    def encode_batch(self, payload, desc, wire=None, wire_cap=None, wire_off=None, stream=None):
+        """Encode frames ``desc`` (uint8 CUDA tensor of n*32 bytes) whose data
+        live in ``payload``.  Returns (wire, wire_off int64[n+1])."""
+        t = self._torch
+        n = int(desc.numel() // SEND_DESC.itemsize)
+        if wire is None:
+            wire = t.empty(max(int(wire_cap), 16), dtype=t.uint8, device=desc.device)
+        cap = int(wire.numel()) if wire_cap is None else int(wire_cap)
+        if wire_off is None:
+            wire_off = t.empty(n + 1, dtype=t.int64, device=desc.device)
+        rc = self._L.wsg_encode_batch(self._ctx, ctypes.c_void_p(payload.data_ptr()),
+                                      ctypes.c_void_p(desc.data_ptr()), n, ctypes.c_void_p(wire.data_ptr()),
+                                      cap, ctypes.c_void_p(wire_off.data_ptr()), self._stream(stream))
+        _check(rc, "wsg_encode_batch")
+        return wire, wire_off
+
+    def fanout(self, payload, keys, opcode, mask=True, wire=None, length=None, stream=None):
+        t = self._torch
+        k = int(keys.numel())
+        length = int(payload.numel()) if length is None else int(length)
+        fsz = frame_size(opcode, mask, length)
+        if wire is None:
+            wire = t.empty(max(fsz * k, 16), dtype=t.uint8, device=payload.device)
+        rc = self._L.wsg_fanout_encode(self._ctx, ctypes.c_void_p(payload.data_ptr()), length,
+                                       ctypes.c_void_p(keys.data_ptr()), k, opcode, 1 if mask else 0,
+                                       ctypes.c_void_p(wire.data_ptr()), wire.numel(), self._stream(stream))
+        _check(rc, "wsg_fanout_encode")
+        return wire
+
+    # -- host-staged paths ----------------------------------------------------
+    def xor_host(self, data, key, phase=0):
+        src = bytes(data)
+        dst = ctypes.create_string_buffer(max(len(src), 1))
+        _check(self._L.wsg_xor_host(self._ctx, src, dst, len(src), key, phase), "wsg_xor_host")
+        return dst.raw[: len(src)]
+
+    def decode_batch_host(self, wire, frame_start):
+        wire = np.ascontiguousarray(wire, dtype=np.uint8)
+        fs = np.ascontiguousarray(frame_start, dtype=np.uint64)
+        out = np.empty(max(len(wire), 1), dtype=np.uint8)
+        info = np.zeros(max(len(fs), 1), dtype=RECV_INFO)
+        rc = self._L.wsg_decode_batch_host(self._ctx, _np_ptr(wire), len(wire), _np_ptr(fs), len(fs),
+                                           _np_ptr(out), _np_ptr(info))
+        return rc, out[: len(wire)], info[: len(fs)]
+
+    # -- measurement hooks ----------------------------------------------------
+    def timing(self, on=True):
+        _check(self._L.wsg_timing_enable(self._ctx, 1 if on else 0), "wsg_timing_enable")
+
+    def timing_read(self, reset=True):
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        _check(self._L.wsg_timing_read(self._ctx, ctypes.byref(ms), ctypes.byref(n), 1 if reset else 0),
+               "wsg_timing_read")
+        return ms.value, n.value
+
+
+def info_to_numpy(info_tensor, n):
+    """Device info bytes -> numpy RECV_INFO records."""
+    return info_tensor[: n * RECV_INFO.itemsize].cpu().numpy().view(RECV_INFO)
+
+
+def desc_to_tensor(desc, device):
+    import torch
+
+    desc = np.ascontiguousarray(desc, dtype=SEND_DESC)
+    return torch.from_numpy(desc.view(np.uint8).copy()).to(device)

@@ -1,0 +1,435 @@
+// wsg_capi.hip — implementation of the C-ABI in include/wsg_capi.h: device
+// context, scratch, batch launches, host-staged paths, timing hooks.
+// Nothing here computes payload bytes on the CPU: every payload byte of
+// every entry point is produced by a gfx950 kernel.
+#include "wsg_internal.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+struct wsg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int num_cus = 256;
+    int blocks_per_cu = 8;
+    unsigned long long* d_err = nullptr;
+    // scratch
+    uint32_t* d_tiles = nullptr;
+    uint64_t tiles_cap = 0;
+    uint64_t* d_scan = nullptr;     // block_sums | block_prefix
+    uint64_t scan_cap = 0;          // entries per half
+    // staging for host entry points
+    uint8_t* d_stage = nullptr;
+    uint8_t* h_stage = nullptr;
+    uint64_t stage_cap = 0;
+    uint64_t* d_fs = nullptr;
+    wsg_recv_info* d_info = nullptr;
+    uint64_t fs_cap = 0;
+    // timing of the dominant kernel
+    struct EvPair {
+        hipEvent_t a, b;
+    };
+    bool timing = false;
+    std::vector<EvPair> pending, pool;
+    double acc_ms = 0.0;
+    uint64_t launches = 0;
+};
+
+namespace {
+
+#define WSG_HIP(expr)                                                                                        \
+    do {                                                                                                     \
+        if ((expr) != hipSuccess)                                                                            \
+            return WSG_EHIP;                                                                                 \
+    } while (0)
+
+constexpr unsigned long long kNoError = ~0ull;
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+// NULL selects HIP's default (null) stream, as in every HIP API.
+inline hipStream_t pick(wsg_ctx*, void* s) { return static_cast<hipStream_t>(s); }
+inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+int grid_for(const wsg_ctx* c, uint64_t tiles)
+{
+    const uint64_t cap = uint64_t(c->num_cus) * uint64_t(c->blocks_per_cu);
+    return int(std::max<uint64_t>(1, std::min(tiles, cap)));
+}
+
+int ensure_tiles(wsg_ctx* c, uint64_t tiles)
+{
+    tiles = std::max<uint64_t>(tiles, 1);
+    if (tiles <= c->tiles_cap)
+        return WSG_OK;
+    WSG_HIP(hipDeviceSynchronize());
+    if (c->d_tiles)
+        WSG_HIP(hipFree(c->d_tiles));
+    c->d_tiles = nullptr;
+    c->tiles_cap = 0;
+    if (hipMalloc(&c->d_tiles, tiles * sizeof(uint32_t)) != hipSuccess)
+        return WSG_ENOMEM;
+    c->tiles_cap = tiles;
+    return WSG_OK;
+}
+
+int ensure_scan(wsg_ctx* c, uint64_t blocks)
+{
+    blocks = std::max<uint64_t>(blocks, 1);
+    if (blocks <= c->scan_cap)
+        return WSG_OK;
+    WSG_HIP(hipDeviceSynchronize());
+    if (c->d_scan)
+        WSG_HIP(hipFree(c->d_scan));
+    c->d_scan = nullptr;
+    c->scan_cap = 0;
+    if (hipMalloc(&c->d_scan, 2 * blocks * sizeof(uint64_t)) != hipSuccess)
+        return WSG_ENOMEM;
+    c->scan_cap = blocks;
+    return WSG_OK;
+}
+
+int ensure_stage(wsg_ctx* c, uint64_t bytes, uint64_t frames)
+{
+    bytes = std::max<uint64_t>((bytes + 15) & ~uint64_t(15), 16);
+    if (bytes > c->stage_cap) {
+        WSG_HIP(hipDeviceSynchronize());
+        if (c->d_stage)
+            WSG_HIP(hipFree(c->d_stage));
+        if (c->h_stage)
+            WSG_HIP(hipHostFree(c->h_stage));
+        c->d_stage = nullptr;
+        c->h_stage = nullptr;
+        c->stage_cap = 0;
+        if (hipMalloc(&c->d_stage, bytes) != hipSuccess)
+            return WSG_ENOMEM;
+        if (hipHostMalloc(&c->h_stage, bytes, hipHostMallocDefault) != hipSuccess)
+            return WSG_ENOMEM;
+        c->stage_cap = bytes;
+    }
+    frames = std::max<uint64_t>(frames, 1);
+    if (frames > c->fs_cap) {
+        WSG_HIP(hipDeviceSynchronize());
+        if (c->d_fs)
+            WSG_HIP(hipFree(c->d_fs));
+        if (c->d_info)
+            WSG_HIP(hipFree(c->d_info));
+        c->d_fs = nullptr;
+        c->d_info = nullptr;
+        c->fs_cap = 0;
+        if (hipMalloc(&c->d_fs, frames * sizeof(uint64_t)) != hipSuccess ||
+            hipMalloc(&c->d_info, frames * sizeof(wsg_recv_info)) != hipSuccess)
+            return WSG_ENOMEM;
+        c->fs_cap = frames;
+    }
+    return WSG_OK;
+}
+
+// Record the start event of a timed kernel; returns the pair index or -1.
+int timing_begin(wsg_ctx* c, hipStream_t s)
+{
+    if (!c->timing)
+        return -1;
+    wsg_ctx::EvPair ev;
+    if (!c->pool.empty()) {
+        ev = c->pool.back();
+        c->pool.pop_back();
+    } else {
+        if (hipEventCreate(&ev.a) != hipSuccess || hipEventCreate(&ev.b) != hipSuccess)
+            return -1;
+    }
+    (void)hipEventRecord(ev.a, s);
+    c->pending.push_back(ev);
+    return int(c->pending.size()) - 1;
+}
+
+void timing_end(wsg_ctx* c, hipStream_t s, int idx)
+{
+    if (idx >= 0)
+        (void)hipEventRecord(c->pending[size_t(idx)].b, s);
+}
+
+int drain_timing(wsg_ctx* c)
+{
+    for (auto& ev : c->pending) {
+        WSG_HIP(hipEventSynchronize(ev.b));
+        float ms = 0.f;
+        WSG_HIP(hipEventElapsedTime(&ms, ev.a, ev.b));
+        c->acc_ms += ms;
+        c->launches += 1;
+        c->pool.push_back(ev);
+    }
+    c->pending.clear();
+    return WSG_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int wsg_abi_version(void) { return WSG_ABI_VERSION; }
+
+const char* wsg_strerror(int code)
+{
+    switch (code) {
+    case WSG_OK:
+        return "ok";
+    case WSG_EINVAL:
+        return "invalid argument or overlapping frames";
+    case WSG_ETRUNC:
+        return "frame runs past the end of the wire";
+    case WSG_ENOMEM:
+        return "out of memory or output capacity too small";
+    case WSG_EHIP:
+        return "HIP runtime error";
+    default:
+        return "unknown error";
+    }
+}
+
+int wsg_create(int device, wsg_ctx** out)
+{
+    if (!out)
+        return WSG_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || device < 0 || device >= count)
+        return WSG_EHIP;
+    wsg_ctx* c = new (std::nothrow) wsg_ctx();
+    if (!c)
+        return WSG_ENOMEM;
+    c->device = device;
+    hipDeviceProp_t prop;
+    if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->d_err, sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_err, 0xFF, sizeof(unsigned long long)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
+        wsg_destroy(c);
+        return WSG_EHIP;
+    }
+    c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (const char* e = std::getenv("WSG_BLOCKS_PER_CU")) {
+        const int v = std::atoi(e);
+        if (v > 0 && v <= 32)
+            c->blocks_per_cu = v;
+    }
+    *out = c;
+    return WSG_OK;
+}
+
+int wsg_destroy(wsg_ctx* c)
+{
+    if (!c)
+        return WSG_EINVAL;
+    (void)hipSetDevice(c->device);
+    if (c->stream)
+        (void)hipStreamSynchronize(c->stream);
+    for (auto& ev : c->pending) {
+        (void)hipEventDestroy(ev.a);
+        (void)hipEventDestroy(ev.b);
+    }
+    for (auto& ev : c->pool) {
+        (void)hipEventDestroy(ev.a);
+        (void)hipEventDestroy(ev.b);
+    }
+    (void)hipFree(c->d_err);
+    (void)hipFree(c->d_tiles);
+    (void)hipFree(c->d_scan);
+    (void)hipFree(c->d_stage);
+    (void)hipFree(c->d_fs);
+    (void)hipFree(c->d_info);
+    if (c->h_stage)
+        (void)hipHostFree(c->h_stage);
+    if (c->stream)
+        (void)hipStreamDestroy(c->stream);
+    delete c;
+    return WSG_OK;
+}
+
+void* wsg_stream(wsg_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
+int wsg_sync(wsg_ctx* c, void* stream)
+{
+    if (!c)
+        return WSG_EINVAL;
+    hipStream_t s = pick(c, stream);
+    unsigned long long e = kNoError;
+    WSG_HIP(hipMemcpyAsync(&e, c->d_err, sizeof(e), hipMemcpyDeviceToHost, s));
+    WSG_HIP(hipStreamSynchronize(s));
+    if (e == kNoError)
+        return WSG_OK;
+    WSG_HIP(hipMemsetAsync(c->d_err, 0xFF, sizeof(unsigned long long), s));
+    WSG_HIP(hipStreamSynchronize(s));
+    return -int(e & 0xFFu);
+}
+
+int wsg_decode_batch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const uint64_t* d_frame_start, uint32_t n,
+                     uint8_t* d_out, wsg_recv_info* d_info, void* stream)
+{
+    if (!c || (wire_len && (!d_wire || !d_out)) || (n && (!d_frame_start || !d_info)))
+        return WSG_EINVAL;
+    if (!aligned16(d_wire) || !aligned16(d_out))
+        return WSG_EINVAL;
+    hipStream_t s = pick(c, stream);
+    if (n == 0) {
+        if (wire_len && d_out != d_wire)
+            WSG_HIP(hipMemcpyAsync(d_out, d_wire, wire_len, hipMemcpyDeviceToDevice, s));
+        return WSG_OK;
+    }
+    const uint64_t tiles = ceil_div(wire_len, wsg::TILE);
+    if (int rc = ensure_tiles(c, tiles))
+        return rc;
+    WSG_HIP(wsg::launch_decode_parse(s, d_wire, wire_len, d_frame_start, n, d_info, c->d_tiles, tiles, c->d_err));
+    if (tiles == 0)
+        return WSG_OK;
+    const int t = timing_begin(c, s);
+    WSG_HIP(wsg::launch_decode_unmask(s, grid_for(c, tiles), d_wire, d_out, wire_len, d_frame_start, d_info, n,
+                                      c->d_tiles, tiles));
+    timing_end(c, s, t);
+    return WSG_OK;
+}
+
+int wsg_encode_batch(wsg_ctx* c, const uint8_t* d_payload, const wsg_send_desc* d_desc, uint32_t n, uint8_t* d_wire,
+                     uint64_t wire_cap, uint64_t* d_wire_off, void* stream)
+{
+    if (!c || !d_wire_off || (n && (!d_desc || !d_wire)))
+        return WSG_EINVAL;
+    if (!aligned16(d_wire))
+        return WSG_EINVAL;
+    hipStream_t s = pick(c, stream);
+    if (n == 0) {
+        WSG_HIP(hipMemsetAsync(d_wire_off, 0, sizeof(uint64_t), s));
+        return WSG_OK;
+    }
+    const uint64_t tiles_cap = ceil_div(wire_cap, wsg::TILE);
+    const uint64_t nb = ceil_div(n, wsg::SCAN_ITEMS);
+    if (int rc = ensure_tiles(c, tiles_cap))
+        return rc;
+    if (int rc = ensure_scan(c, nb))
+        return rc;
+    WSG_HIP(wsg::launch_encode_scan(s, d_desc, n, d_wire_off, c->d_scan, c->d_scan + c->scan_cap, c->d_tiles,
+                                    tiles_cap, wire_cap, c->d_err));
+    const int t = timing_begin(c, s);
+    WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, tiles_cap), d_payload, d_desc, n, d_wire_off, c->d_tiles, d_wire,
+                                    wire_cap));
+    timing_end(c, s, t);
+    return WSG_OK;
+}
+
+int wsg_fanout_encode(wsg_ctx* c, const uint8_t* d_payload, uint64_t len, const uint32_t* d_keys, uint32_t k,
+                      uint8_t opcode, int mask, uint8_t* d_wire, uint64_t wire_cap, void* stream)
+{
+    if (!c || (k && (!d_keys || !d_wire)) || (len && !d_payload))
+        return WSG_EINVAL;
+    if (!aligned16(d_wire))
+        return WSG_EINVAL;
+    if (k == 0)
+        return WSG_OK;
+    const uint64_t fsize = wsg_frame_size(opcode, mask, len, 0);
+    const uint64_t total = fsize * k;
+    if (total > wire_cap)
+        return WSG_ENOMEM;
+    hipStream_t s = pick(c, stream);
+    const int t = timing_begin(c, s);
+    WSG_HIP(wsg::launch_fanout(s, grid_for(c, ceil_div(total, wsg::TILE)), d_payload, len, d_keys, k, opcode,
+                               mask ? 1u : 0u, fsize, d_wire));
+    timing_end(c, s, t);
+    return WSG_OK;
+}
+
+int wsg_xor_host(wsg_ctx* c, const void* src, void* dst, size_t len, uint32_t key, uint32_t phase)
+{
+    if (!c || (len && (!src || !dst)))
+        return WSG_EINVAL;
+    if (len == 0)
+        return WSG_OK;
+    if (int rc = ensure_stage(c, len, 0))
+        return rc;
+    hipStream_t s = c->stream;
+    std::memcpy(c->h_stage, src, len);
+    WSG_HIP(hipMemcpyAsync(c->d_stage, c->h_stage, len, hipMemcpyHostToDevice, s));
+    const uint64_t chunks = ceil_div(len, wsg::CHUNK);
+    WSG_HIP(wsg::launch_xor(s, grid_for(c, ceil_div(chunks, wsg::BLOCK)), c->d_stage, c->d_stage, len, key, phase));
+    WSG_HIP(hipMemcpyAsync(c->h_stage, c->d_stage, len, hipMemcpyDeviceToHost, s));
+    WSG_HIP(hipStreamSynchronize(s));
+    std::memcpy(dst, c->h_stage, len);
+    return WSG_OK;
+}
+
+int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start,
+                          uint32_t n, uint8_t* out, wsg_recv_info* info)
+{
+    if (!c || (wire_len && (!wire || !out)) || (n && (!frame_start || !info)))
+        return WSG_EINVAL;
+    if (int rc = ensure_stage(c, wire_len, n))
+        return rc;
+    hipStream_t s = c->stream;
+    WSG_HIP(hipMemcpyAsync(c->d_stage, wire, wire_len, hipMemcpyHostToDevice, s));
+    if (n)
+        WSG_HIP(hipMemcpyAsync(c->d_fs, frame_start, n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    if (int rc = wsg_decode_batch(c, c->d_stage, wire_len, c->d_fs, n, c->d_stage, c->d_info, s))
+        return rc;
+    WSG_HIP(hipMemcpyAsync(out, c->d_stage, wire_len, hipMemcpyDeviceToHost, s));
+    if (n)
+        WSG_HIP(hipMemcpyAsync(info, c->d_info, n * sizeof(wsg_recv_info), hipMemcpyDeviceToHost, s));
+    return wsg_sync(c, s);
+}
+
+uint64_t wsg_frame_size(uint8_t opcode, int mask, uint64_t len, int32_t status)
+{
+    const wsg::SendGeom g = wsg::send_geom(opcode, mask != 0, len, status);
+    return g.hdr + g.body;
+}
+
+int wsg_header_pack(uint8_t opcode, int mask, uint64_t len, int32_t status, uint32_t key, uint8_t* out)
+{
+    if (!out)
+        return WSG_EINVAL;
+    const wsg::SendGeom g = wsg::send_geom(opcode, mask != 0, len, status);
+    for (uint32_t r = 0; r < g.hdr; ++r)
+        out[r] = wsg::header_byte(opcode, mask != 0, g.body, key, r);
+    return int(g.hdr);
+}
+
+int wsg_header_unpack(const uint8_t* buf, uint64_t avail, wsg_recv_info* info)
+{
+    if (!info || (avail && !buf))
+        return WSG_EINVAL;
+    wsg_recv_info r = {};
+    const int e = wsg::parse_header([&](uint32_t k) { return buf[k]; }, avail, r);
+    if (e)
+        return e;
+    r.payload_off = r.hdr_len;
+    *info = r;
+    return WSG_OK;
+}
+
+int wsg_timing_enable(wsg_ctx* c, int on)
+{
+    if (!c)
+        return WSG_EINVAL;
+    c->timing = on != 0;
+    return WSG_OK;
+}
+
+int wsg_timing_read(wsg_ctx* c, double* total_ms, uint64_t* launches, int reset)
+{
+    if (!c)
+        return WSG_EINVAL;
+    if (int rc = drain_timing(c))
+        return rc;
+    if (total_ms)
+        *total_ms = c->acc_ms;
+    if (launches)
+        *launches = c->launches;
+    if (reset) {
+        c->acc_ms = 0.0;
+        c->launches = 0;
+    }
+    return WSG_OK;
+}
+
+} // extern "C"

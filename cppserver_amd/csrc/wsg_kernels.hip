@@ -1,0 +1,779 @@
+// wsg_kernels.hip — gfx950 (CDNA4) kernels for batched WebSocket frame
+// decode (header unpack + payload unmask) and encode (header pack + payload
+// mask), the per-byte hot path of CppServer's WebSocket codec
+// (reference source/server/ws/ws.cpp:212-456).
+//
+// Layout in HBM:
+//   decode: wire (concatenated frames) -> out (same geometry, payloads
+//           unmasked where they sit); per-frame wsg_recv_info.
+//   encode: payload arena + wsg_send_desc[] -> wire (frames back to back).
+// Work unit: a 16 KiB tile of the OUTPUT byte range = 256 lanes x 16 B x 4.
+// Every output byte is written exactly once by an aligned 16-byte
+// nontemporal store (output is streamed, never re-read by the kernel).
+//
+// Three tile paths, chosen per tile (wave-uniform branch):
+//   stream   - the tile lies inside one payload: one 16-B load, four XORs
+//              with a tile-uniform rotated key, one 16-B store per step;
+//   boundary - the tile touches <= MAXF frames: their records are held in
+//              (scalar) registers and each 16-B chunk is classified against
+//              them; only chunks holding a header byte go byte-by-byte;
+//   dense    - more frames than that (tiny frames): per-chunk binary search
+//              of the frame table.
+// No MFMA: XOR is not a contraction; the bound is HBM bandwidth.
+#include "wsg_internal.h"
+
+namespace wsg {
+
+namespace {
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint64_t v4u64 __attribute__((ext_vector_type(4)));   // MAXF-wide frame fields
+
+constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary path
+
+__device__ __forceinline__ v4u ld16(const uint8_t* p) { return *reinterpret_cast<const v4u*>(p); }
+__device__ __forceinline__ v4u ld16nt(const uint8_t* p)
+{
+    return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+}
+__device__ __forceinline__ void st16nt(uint8_t* p, v4u v) { __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p)); }
+
+__device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t b)
+{
+    return __builtin_amdgcn_alignbyte(hi, lo, b);   // ({hi,lo} >> 8b)[31:0]
+}
+
+// Bytes [s, s+16) of the 32-byte little-endian window lo:hi (v_alignbyte_b32).
+__device__ __forceinline__ v4u funnel(v4u lo, v4u hi, uint32_t s)
+{
+    const uint32_t b = s & 3u;
+    v4u r;
+    switch (s >> 2) {
+    case 0:
+        r = v4u{ab(lo.y, lo.x, b), ab(lo.z, lo.y, b), ab(lo.w, lo.z, b), ab(hi.x, lo.w, b)};
+        break;
+    case 1:
+        r = v4u{ab(lo.z, lo.y, b), ab(lo.w, lo.z, b), ab(hi.x, lo.w, b), ab(hi.y, hi.x, b)};
+        break;
+    case 2:
+        r = v4u{ab(lo.w, lo.z, b), ab(hi.x, lo.w, b), ab(hi.y, hi.x, b), ab(hi.z, hi.y, b)};
+        break;
+    default:
+        r = v4u{ab(hi.x, lo.w, b), ab(hi.y, hi.x, b), ab(hi.z, hi.y, b), ab(hi.w, hi.z, b)};
+        break;
+    }
+    return r;
+}
+
+// 16 source bytes at an arbitrary address, read as aligned 16-B blocks
+// (never touching a 16-B block that holds no requested byte).
+template <bool NT>
+__device__ __forceinline__ v4u ld16_unaligned(const uint8_t* a)
+{
+    const uint32_t s = uint32_t(reinterpret_cast<uintptr_t>(a) & 15u);
+    const uint8_t* a0 = a - s;
+    const v4u lo = NT ? ld16nt(a0) : ld16(a0);
+    if (s == 0)
+        return lo;
+    return funnel(lo, NT ? ld16nt(a0 + 16) : ld16(a0 + 16), s);
+}
+
+// Byte j (runtime) of a 16-byte value, through two 64-bit halves so that no
+// register array is indexed at run time (that would spill to scratch).
+__device__ __forceinline__ uint32_t lane_byte(v4u v, uint32_t j)
+{
+    const uint64_t lo = uint64_t(v.x) | (uint64_t(v.y) << 32);
+    const uint64_t hi = uint64_t(v.z) | (uint64_t(v.w) << 32);
+    return uint32_t((j < 8 ? lo >> (8u * j) : hi >> (8u * (j - 8))) & 0xFFu);
+}
+
+__device__ __forceinline__ void put_byte(v4u& w, uint32_t j, uint32_t b)
+{
+    const uint64_t m = uint64_t(b & 0xFFu) << (8u * (j & 7u));
+    const uint64_t lo = j < 8 ? m : 0, hi = j < 8 ? 0 : m;
+    w.x |= uint32_t(lo);
+    w.y |= uint32_t(lo >> 32);
+    w.z |= uint32_t(hi);
+    w.w |= uint32_t(hi >> 32);
+}
+
+// v[j] for a runtime j < MAXF, as a select chain (no scratch).
+template <class V>
+__device__ __forceinline__ auto pick(V v, int j) -> decltype(v[0] + 0)
+{
+    auto r = v[0];
+    r = (j == 1) ? v[1] : r;
+    r = (j == 2) ? v[2] : r;
+    r = (j == 3) ? v[3] : r;
+    return r;
+}
+
+__device__ __forceinline__ void store_partial(uint8_t* dst, v4u w, uint32_t nbytes)
+{
+    for (uint32_t j = 0; j < nbytes; ++j)
+        dst[j] = uint8_t(lane_byte(w, j));
+}
+
+__device__ __forceinline__ uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+__device__ __forceinline__ uint64_t lane_off(int u) { return (uint64_t(u) * BLOCK + threadIdx.x) * CHUNK; }
+
+// Last index in [lo, hi] whose start <= p; lo - 1 (possibly -1) if none.
+__device__ __forceinline__ int64_t owner_search(const uint64_t* start, int64_t lo, int64_t hi, uint64_t p)
+{
+    if (start[lo] > p)
+        return lo - 1;
+    while (lo < hi) {
+        const int64_t mid = lo + ((hi - lo + 1) >> 1);
+        if (start[mid] <= p)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
+// ---- wave / block exclusive scan of uint64 (wave64) ----------------------
+__device__ __forceinline__ uint64_t wave_inclusive_scan(uint64_t v)
+{
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t u = __shfl_up(v, d, 64);
+        if (lane >= d)
+            v += u;
+    }
+    return v;
+}
+
+// Exclusive scan over the block (blockDim.x == BLOCK); *total = block sum.
+__device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total)
+{
+    __shared__ uint64_t wsum[BLOCK / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t inc = wave_inclusive_scan(v);
+    if (lane == 63)
+        wsum[wid] = inc;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int k = 0; k < BLOCK / 64; ++k) {
+        before += (k < wid) ? wsum[k] : 0;
+        all += wsum[k];
+    }
+    __syncthreads();
+    *total = all;
+    return before + inc - v;
+}
+
+} // namespace
+
+// ===========================================================================
+// Decode
+// ===========================================================================
+
+// One lane per frame: header unpack (ws.cpp:320-386) from one 16-byte window
+// read, bounds checks, and the tile -> first-frame map of the unmask kernel.
+__global__ __launch_bounds__(BLOCK) void k_decode_parse(const uint8_t* __restrict__ wire, uint64_t wire_len,
+                                                        const uint64_t* __restrict__ fs, uint32_t n,
+                                                        wsg_recv_info* __restrict__ info,
+                                                        uint32_t* __restrict__ tile_first, uint64_t num_tiles,
+                                                        unsigned long long* err)
+{
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint64_t s = fs[i];
+    const uint64_t limit = (i + 1 < n) ? fs[i + 1] : wire_len;
+    wsg_recv_info r = {};
+    int e = WSG_ETRUNC;
+    if (s < wire_len) {
+        const uint64_t avail = wire_len - s;
+        const uint64_t a0 = s & ~uint64_t(15);
+        const v4u lo = ld16(wire + a0);
+        const v4u hi = (a0 + 16 < wire_len) ? ld16(wire + a0 + 16) : v4u{0, 0, 0, 0};
+        const v4u h = funnel(lo, hi, uint32_t(s & 15));   // wire[s .. s+16)
+        e = parse_header([&](uint32_t k) { return uint8_t(lane_byte(h, k)); }, avail, r);
+        if (e == 0) {
+            if (r.len > avail - r.hdr_len)
+                e = WSG_ETRUNC;
+            else if (limit < s || limit - s < r.hdr_len || r.len > limit - s - r.hdr_len)
+                e = WSG_EINVAL;   // the next frame starts inside this one
+        }
+    }
+    if (e != 0) {
+        r = wsg_recv_info{};
+        r.payload_off = s;
+        r.error = int8_t(e);
+        atomicMin(err, (static_cast<unsigned long long>(i) << 8) | static_cast<unsigned long long>(-e));
+    } else {
+        r.payload_off = s + r.hdr_len;
+    }
+    info[i] = r;
+
+    // tiles whose first byte falls in [s, next start) belong to frame i
+    const uint64_t lo_t = (i == 0) ? 0 : ceil_div(s, TILE);
+    uint64_t hi_t = (i + 1 < n) ? ceil_div(limit, TILE) : num_tiles;
+    if (hi_t > num_tiles)
+        hi_t = num_tiles;
+    for (uint64_t t = lo_t; t < hi_t; ++t)
+        tile_first[t] = i;
+}
+
+namespace {
+
+// Generic chunk of the unmask: owner by binary search, byte loop at frame
+// boundaries.  Used by dense tiles (many tiny frames) and the wire's tail.
+__device__ __forceinline__ void decode_chunk_generic(const uint8_t* __restrict__ wire, uint8_t* out, uint64_t wire_len,
+                                     const uint64_t* __restrict__ fs, const wsg_recv_info* __restrict__ info,
+                                     uint32_t n, uint32_t f, uint32_t f_hi, uint64_t p)
+{
+    int64_t o = owner_search(fs, f, f_hi, p);
+    uint64_t opoff = 0, oplen = 0;
+    uint32_t okey = 0;
+    if (o >= 0) {
+        opoff = info[o].payload_off;
+        oplen = info[o].len;
+        okey = info[o].key;
+        if (p >= opoff && p + CHUNK <= opoff + oplen) {
+            st16nt(out + p, ld16(wire + p) ^ key_rot(okey, uint32_t(p - opoff)));
+            return;
+        }
+    }
+    const uint32_t nb = uint32_t(min<uint64_t>(CHUNK, wire_len - p));
+    v4u w = {0, 0, 0, 0};
+    for (uint32_t j = 0; j < nb; ++j) {
+        const uint64_t q = p + j;
+        while (o + 1 < int64_t(n) && fs[o + 1] <= q) {
+            ++o;
+            opoff = info[o].payload_off;
+            oplen = info[o].len;
+            okey = info[o].key;
+        }
+        uint32_t b = wire[q];
+        if (o >= 0 && q >= opoff && q - opoff < oplen)
+            b ^= key_byte(okey, q - opoff);
+        put_byte(w, j, b);
+    }
+    if (nb == CHUNK)
+        st16nt(out + p, w);
+    else
+        store_partial(out + p, w, nb);
+}
+
+// Records of the (at most MAXF) frames a boundary tile touches, as vector
+// values (kept in registers; MAXF == 4 == vector width).
+struct DecFrames {
+    v4u64 st;   // frame start (~0 when absent)
+    v4u64 po;   // payload start
+    v4u64 pe;   // payload end
+    v4u key;
+};
+static_assert(MAXF == 4, "frame records are 4-wide vectors");
+
+__device__ __forceinline__ int dec_owner(const DecFrames& F, uint64_t q)
+{
+    int j = -1;
+#pragma unroll
+    for (int k = 0; k < MAXF; ++k)
+        j = (F.st[k] <= q) ? k : j;
+    return j;
+}
+
+} // namespace
+
+// Unmask (ws.cpp:399-406): out = wire with every payload XORed by its key.
+__global__ __launch_bounds__(BLOCK) void k_decode_unmask(const uint8_t* __restrict__ wire, uint8_t* out,
+                                                         uint64_t wire_len, const uint64_t* __restrict__ fs,
+                                                         const wsg_recv_info* __restrict__ info, uint32_t n,
+                                                         const uint32_t* __restrict__ tile_first,
+                                                         uint64_t num_tiles)
+{
+    for (uint64_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
+        const uint64_t base = t * TILE;
+        const uint64_t tend = min(base + TILE, wire_len);
+        const uint32_t f = min(tile_first[t], n - 1);
+        uint32_t f_hi = (t + 1 < num_tiles) ? min(tile_first[t + 1], n - 1) : n - 1;
+        f_hi = max(f, f_hi);   // f_hi < f only with invalid (non-monotone) frame starts
+
+        if (tend - base != TILE) {
+            // the wire's last, partial tile
+#pragma unroll 1
+            for (int u = 0; u < UNROLL; ++u) {
+                const uint64_t p = base + lane_off(u);
+                if (p < tend)
+                    decode_chunk_generic(wire, out, wire_len, fs, info, n, f, f_hi, p);
+            }
+            continue;
+        }
+
+        // the tile's data does not depend on frame metadata: issue it first
+        v4u v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+            v[u] = ld16nt(wire + base + lane_off(u));
+
+        const uint64_t poff = info[f].payload_off;
+        const uint64_t pend = poff + info[f].len;
+        const uint32_t key = info[f].key;
+        if (base >= poff && tend <= pend) {
+            // stream: the whole tile is payload of frame f
+            const uint32_t k = key_rot(key, uint32_t(base - poff));
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u)
+                st16nt(out + base + lane_off(u), v[u] ^ k);
+            continue;
+        }
+
+        if (f_hi - f < MAXF) {
+            // boundary: frames f..f_hi from registers
+            DecFrames F;
+#pragma unroll
+            for (int k = 0; k < MAXF; ++k) {
+                if (f + k <= f_hi) {
+                    F.st[k] = fs[f + k];
+                    F.po[k] = info[f + k].payload_off;
+                    F.pe[k] = F.po[k] + info[f + k].len;
+                    F.key[k] = info[f + k].key;
+                } else {
+                    F.st[k] = ~uint64_t(0);
+                    F.po[k] = F.pe[k] = 0;
+                    F.key[k] = 0;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const uint64_t p = base + lane_off(u);
+                const int j = dec_owner(F, p);
+                const uint64_t po = pick(F.po, j < 0 ? 0 : j), pe = pick(F.pe, j < 0 ? 0 : j);
+                if (j >= 0 && p >= po && p + CHUNK <= pe) {
+                    st16nt(out + p, v[u] ^ key_rot(pick(F.key, j), uint32_t(p - po)));
+                } else {
+                    v4u w = v[u];
+#pragma unroll
+                    for (uint32_t b = 0; b < CHUNK; ++b) {
+                        const uint64_t q = p + b;
+                        const int jb = dec_owner(F, q);
+                        const int jc = jb < 0 ? 0 : jb;
+                        const uint64_t qo = pick(F.po, jc);
+                        if (jb >= 0 && q >= qo && q < pick(F.pe, jc))
+                            w[b >> 2] ^= uint32_t(key_byte(pick(F.key, jc), q - qo)) << (8u * (b & 3u));
+                    }
+                    st16nt(out + p, w);
+                }
+            }
+            continue;
+        }
+
+        // dense: many tiny frames in this tile
+#pragma unroll 1
+        for (int u = 0; u < UNROLL; ++u)
+            decode_chunk_generic(wire, out, wire_len, fs, info, n, f, f_hi, base + lane_off(u));
+    }
+}
+
+// ===========================================================================
+// Encode
+// ===========================================================================
+
+namespace {
+
+// Everything the mask kernel needs about one output frame.
+struct FrameRec {
+    uint64_t off;       // wire offset of the frame
+    uint64_t pw;        // wire offset of the payload (status prefix included)
+    uint64_t data_w;    // wire offset of the first data byte
+    uint64_t end;       // wire offset one past the frame
+    const uint8_t* src; // data bytes
+    uint64_t body;
+    uint32_t key;
+    uint32_t hdr;
+    uint32_t prefix;
+    int32_t status;
+    uint8_t opcode;
+    bool mask;
+};
+
+__device__ __forceinline__ FrameRec make_rec(uint64_t off, const uint8_t* src, uint64_t len, uint32_t key,
+                                             int32_t status, uint8_t opcode, bool mask)
+{
+    const SendGeom g = send_geom(opcode, mask, len, status);
+    FrameRec r;
+    r.off = off;
+    r.pw = off + g.hdr;
+    r.data_w = r.pw + g.prefix;
+    r.end = r.pw + g.body;
+    r.src = src;
+    r.body = g.body;
+    r.key = key;
+    r.hdr = g.hdr;
+    r.prefix = g.prefix;
+    r.status = status;
+    r.opcode = opcode;
+    r.mask = mask;
+    return r;
+}
+
+// Frames described by wsg_send_desc[] with scanned wire offsets.
+struct DescLayout {
+    static constexpr bool kNtSource = true;   // each payload byte is read once
+    const uint8_t* payload;
+    const wsg_send_desc* desc;
+    const uint64_t* wire_off;   // n + 1 entries
+    const uint32_t* tile_first;
+    uint32_t n;
+
+    __device__ FrameRec rec(int64_t o) const
+    {
+        const wsg_send_desc d = desc[o];
+        return make_rec(wire_off[o], payload + d.src_off, d.len, d.key, d.status, d.opcode, d.mask != 0);
+    }
+    __device__ int64_t first(uint64_t t) const { return min(tile_first[t], n - 1); }
+    __device__ int64_t owner(uint64_t p, int64_t f, int64_t f_hi) const { return owner_search(wire_off, f, f_hi, p); }
+    __device__ int64_t last_in_tile(uint64_t t, uint64_t num_tiles, int64_t f, uint64_t) const
+    {
+        int64_t h = (t + 1 < num_tiles) ? int64_t(min(tile_first[t + 1], n - 1)) : int64_t(n) - 1;
+        return h < f ? f : h;
+    }
+};
+
+// k frames of one payload, one key each (client-style fan-out).
+struct FanoutLayout {
+    static constexpr bool kNtSource = false;  // the payload is re-read by every frame: keep it in L2
+    const uint8_t* payload;
+    const uint32_t* keys;
+    uint64_t len;
+    uint64_t fsize;
+    double inv_fsize;
+    uint32_t n;
+    uint8_t opcode;
+    bool mask;
+
+    __device__ FrameRec rec(int64_t o) const
+    {
+        return make_rec(uint64_t(o) * fsize, payload, len, keys[o], 0, opcode, mask);
+    }
+    __device__ int64_t div(uint64_t p) const
+    {
+        int64_t o = int64_t(double(p) * inv_fsize);
+        if (o > 0 && uint64_t(o) * fsize > p)
+            --o;
+        if (uint64_t(o + 1) * fsize <= p)
+            ++o;
+        return o < int64_t(n) ? o : int64_t(n) - 1;
+    }
+    __device__ int64_t first(uint64_t t) const { return div(t * TILE); }
+    __device__ int64_t owner(uint64_t p, int64_t, int64_t) const { return div(p); }
+    __device__ int64_t last_in_tile(uint64_t, uint64_t, int64_t, uint64_t tend) const { return div(tend - 1); }
+};
+
+// One 16-byte output chunk of frame o (or of the frames after it).
+template <class L>
+__device__ __forceinline__ void encode_chunk(const L& lay, uint8_t* wire, uint64_t p, uint64_t total, int64_t o)
+{
+    FrameRec R = lay.rec(o);
+    if (p >= R.data_w && p + CHUNK <= R.end) {
+        const v4u v = ld16_unaligned<L::kNtSource>(R.src + (p - R.data_w));
+        st16nt(wire + p, v ^ key_rot(R.key, uint32_t(p - R.pw)));
+        return;
+    }
+    const uint32_t nb = uint32_t(min<uint64_t>(CHUNK, total - p));
+    v4u w = {0, 0, 0, 0};
+    for (uint32_t j = 0; j < nb; ++j) {
+        const uint64_t q = p + j;
+        while (q >= R.end && o + 1 < int64_t(lay.n)) {
+            ++o;
+            R = lay.rec(o);
+        }
+        const uint64_t r = q - R.off;
+        uint32_t b;
+        if (r < R.hdr) {
+            b = header_byte(R.opcode, R.mask, R.body, R.key, uint32_t(r));
+        } else {
+            const uint64_t k = r - R.hdr;   // payload position (key index)
+            if (k < R.prefix)
+                b = uint32_t((k == 0 ? (R.status >> 8) : R.status) & 0xFF) ^ key_byte(R.key, k);
+            else
+                b = uint32_t(R.src[k - R.prefix]) ^ key_byte(R.key, k);
+        }
+        put_byte(w, j, b);
+    }
+    if (nb == CHUNK)
+        st16nt(wire + p, w);
+    else
+        store_partial(wire + p, w, nb);
+}
+
+// What the boundary path keeps per frame (data-chunk test and source).
+struct EncFrames {
+    v4u64 st;    // frame start (~0 when absent)
+    v4u64 dw;    // first data byte
+    v4u64 end;   // one past the frame
+    v4u64 pw;    // payload start (key phase origin)
+    v4u64 sb;    // address of (src - data_w): source of wire byte q is sb + q
+    v4u key;
+};
+
+template <class L>
+__device__ __forceinline__ void encode_tiles(const L& lay, uint8_t* wire, uint64_t total)
+{
+    const uint64_t num_tiles = (total + TILE - 1) / TILE;
+    for (uint64_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
+        const uint64_t base = t * TILE;
+        const uint64_t tend = min(base + TILE, total);
+        const bool full = (tend - base == TILE);
+        const int64_t f = lay.first(t);
+        const FrameRec R = lay.rec(f);
+        if (full && base >= R.data_w && tend <= R.end) {
+            // stream: the whole tile is data of frame f (uniform shift and key)
+            const uint8_t* src = R.src + (base - R.data_w);
+            const uint32_t k = key_rot(R.key, uint32_t(base - R.pw));
+            const uint32_t s = uint32_t(reinterpret_cast<uintptr_t>(src) & 15u);
+            const uint8_t* a0 = src - s;
+            v4u lo[UNROLL];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u)
+                lo[u] = L::kNtSource ? ld16nt(a0 + lane_off(u)) : ld16(a0 + lane_off(u));
+            if (s != 0) {
+                v4u hi[UNROLL];
+#pragma unroll
+                for (int u = 0; u < UNROLL; ++u)
+                    hi[u] = L::kNtSource ? ld16nt(a0 + lane_off(u) + CHUNK) : ld16(a0 + lane_off(u) + CHUNK);
+#pragma unroll
+                for (int u = 0; u < UNROLL; ++u)
+                    lo[u] = funnel(lo[u], hi[u], s);
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u)
+                st16nt(wire + base + lane_off(u), lo[u] ^ k);
+            continue;
+        }
+        const int64_t f_hi = lay.last_in_tile(t, num_tiles, f, tend);
+        if (full && f_hi - f < MAXF) {
+            // boundary: frames f..f_hi from registers
+            EncFrames F;
+#pragma unroll
+            for (int k = 0; k < MAXF; ++k) {
+                if (f + k <= f_hi) {
+                    const FrameRec Rk = (k == 0) ? R : lay.rec(f + k);
+                    F.st[k] = Rk.off;
+                    F.dw[k] = Rk.data_w;
+                    F.end[k] = Rk.end;
+                    F.pw[k] = Rk.pw;
+                    F.sb[k] = reinterpret_cast<uintptr_t>(Rk.src) - Rk.data_w;
+                    F.key[k] = Rk.key;
+                } else {
+                    F.st[k] = ~uint64_t(0);
+                    F.dw[k] = F.end[k] = F.pw[k] = 0;
+                    F.sb[k] = 0;
+                    F.key[k] = 0;
+                }
+            }
+            // all source loads of the lane first, then the stores
+            v4u v[UNROLL];
+            int js[UNROLL];
+            bool data[UNROLL];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const uint64_t p = base + lane_off(u);
+                int j = 0;
+#pragma unroll
+                for (int k = 1; k < MAXF; ++k)
+                    j = (F.st[k] <= p) ? k : j;
+                js[u] = j;
+                data[u] = p >= pick(F.dw, j) && p + CHUNK <= pick(F.end, j);
+                v[u] = data[u] ? ld16_unaligned<L::kNtSource>(reinterpret_cast<const uint8_t*>(pick(F.sb, j) + p)) : v4u{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const uint64_t p = base + lane_off(u);
+                const int j = js[u];
+                if (data[u])
+                    st16nt(wire + p, v[u] ^ key_rot(pick(F.key, j), uint32_t(p - pick(F.pw, j))));
+                else
+                    encode_chunk(lay, wire, p, total, f + j);   // header bytes: rare
+            }
+            continue;
+        }
+        // dense tiles and the last partial tile
+#pragma unroll 1
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t p = base + lane_off(u);
+            if (p >= tend)
+                break;
+            encode_chunk(lay, wire, p, total, lay.owner(p, f, f_hi));
+        }
+    }
+}
+
+} // namespace
+
+// Per-block local exclusive scan of frame sizes (SCAN_ITEMS frames / block).
+__global__ __launch_bounds__(BLOCK) void k_encode_scan_local(const wsg_send_desc* __restrict__ desc, uint32_t n,
+                                                             uint64_t* __restrict__ wire_off,
+                                                             uint64_t* __restrict__ block_sums)
+{
+    const uint64_t first = uint64_t(blockIdx.x) * SCAN_ITEMS + uint64_t(threadIdx.x) * SCAN_PER_LANE;
+    uint64_t sz[SCAN_PER_LANE];
+    uint64_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER_LANE; ++k) {
+        const uint64_t i = first + k;
+        sz[k] = 0;
+        if (i < n) {
+            const wsg_send_desc d = desc[i];
+            const SendGeom g = send_geom(d.opcode, d.mask != 0, d.len, d.status);
+            sz[k] = g.hdr + g.body;
+        }
+        mine += sz[k];
+    }
+    uint64_t total;
+    uint64_t run = block_exclusive_scan(mine, &total);
+#pragma unroll
+    for (int k = 0; k < SCAN_PER_LANE; ++k) {
+        const uint64_t i = first + k;
+        if (i < n)
+            wire_off[i] = run;
+        run += sz[k];
+    }
+    if (threadIdx.x == 0)
+        block_sums[blockIdx.x] = total;
+}
+
+// Single block: exclusive scan of the block sums; wire_off[n] = total.
+__global__ __launch_bounds__(BLOCK) void k_encode_scan_blocks(const uint64_t* __restrict__ block_sums, uint32_t nb,
+                                                              uint64_t* __restrict__ block_prefix,
+                                                              uint64_t* __restrict__ wire_off, uint32_t n)
+{
+    uint64_t carry = 0;
+    for (uint32_t c = 0; c < nb; c += BLOCK) {
+        const uint32_t i = c + threadIdx.x;
+        const uint64_t v = i < nb ? block_sums[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(v, &tot);
+        if (i < nb)
+            block_prefix[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0)
+        wire_off[n] = carry;
+}
+
+// Add block prefixes, build the tile -> first-frame map, check capacity.
+__global__ __launch_bounds__(BLOCK) void k_encode_finalize(const wsg_send_desc* __restrict__ desc, uint32_t n,
+                                                           uint64_t* __restrict__ wire_off,
+                                                           const uint64_t* __restrict__ block_prefix,
+                                                           uint32_t* __restrict__ tile_first, uint64_t tiles_cap,
+                                                           uint64_t wire_cap, unsigned long long* err)
+{
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n)
+        return;
+    const wsg_send_desc d = desc[i];
+    const SendGeom g = send_geom(d.opcode, d.mask != 0, d.len, d.status);
+    const uint64_t off = wire_off[i] + block_prefix[i / SCAN_ITEMS];
+    const uint64_t end = off + g.hdr + g.body;
+    wire_off[i] = off;
+    if (end > wire_cap)
+        atomicMin(err, (static_cast<unsigned long long>(i) << 8) | static_cast<unsigned long long>(-WSG_ENOMEM));
+    const uint64_t lo = (i == 0) ? 0 : ceil_div(off, TILE);
+    uint64_t hi = ceil_div(end, TILE);
+    if (hi > tiles_cap)
+        hi = tiles_cap;
+    for (uint64_t t = lo; t < hi; ++t)
+        tile_first[t] = i;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_encode_mask(const uint8_t* __restrict__ payload,
+                                                       const wsg_send_desc* __restrict__ desc, uint32_t n,
+                                                       const uint64_t* __restrict__ wire_off,
+                                                       const uint32_t* __restrict__ tile_first,
+                                                       uint8_t* __restrict__ wire, uint64_t wire_cap)
+{
+    const uint64_t total = wire_off[n];
+    if (total > wire_cap)
+        return;   // capacity error latched by k_encode_finalize
+    DescLayout lay{payload, desc, wire_off, tile_first, n};
+    encode_tiles(lay, wire, total);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_fanout(const uint8_t* __restrict__ payload, uint64_t len,
+                                                  const uint32_t* __restrict__ keys, uint32_t k, uint8_t opcode,
+                                                  uint32_t mask, uint64_t fsize, double inv_fsize,
+                                                  uint8_t* __restrict__ wire)
+{
+    FanoutLayout lay{payload, keys, len, fsize, inv_fsize, k, opcode, mask != 0};
+    encode_tiles(lay, wire, fsize * k);
+}
+
+// Single-buffer XOR used by the per-frame host path: dst[i] = src[i] ^
+// key[(phase + i) % 4].  src/dst 16-byte aligned device staging buffers.
+__global__ __launch_bounds__(BLOCK) void k_xor(const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,
+                                               uint32_t phase)
+{
+    const uint32_t k = key_rot(key, phase);
+    const uint64_t chunks = len / CHUNK;
+    for (uint64_t c = uint64_t(blockIdx.x) * BLOCK + threadIdx.x; c < chunks; c += uint64_t(gridDim.x) * BLOCK)
+        *reinterpret_cast<v4u*>(dst + c * CHUNK) = ld16(src + c * CHUNK) ^ k;
+    if (blockIdx.x == 0 && threadIdx.x < (len & (CHUNK - 1))) {
+        const uint64_t q = chunks * CHUNK + threadIdx.x;
+        dst[q] = src[q] ^ key_byte(key, phase + q);
+    }
+}
+
+// ===========================================================================
+// Host launchers
+// ===========================================================================
+
+hipError_t launch_decode_parse(hipStream_t s, const uint8_t* wire, uint64_t wire_len, const uint64_t* fs, uint32_t n,
+                               wsg_recv_info* info, uint32_t* tile_first, uint64_t num_tiles,
+                               unsigned long long* err)
+{
+    const uint32_t grid = (n + BLOCK - 1) / BLOCK;
+    k_decode_parse<<<grid, BLOCK, 0, s>>>(wire, wire_len, fs, n, info, tile_first, num_tiles, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_unmask(hipStream_t s, int grid, const uint8_t* wire, uint8_t* out, uint64_t wire_len,
+                                const uint64_t* fs, const wsg_recv_info* info, uint32_t n,
+                                const uint32_t* tile_first, uint64_t num_tiles)
+{
+    k_decode_unmask<<<grid, BLOCK, 0, s>>>(wire, out, wire_len, fs, info, n, tile_first, num_tiles);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_scan(hipStream_t s, const wsg_send_desc* desc, uint32_t n, uint64_t* wire_off,
+                              uint64_t* block_sums, uint64_t* block_prefix, uint32_t* tile_first,
+                              uint64_t tiles_cap, uint64_t wire_cap, unsigned long long* err)
+{
+    const uint32_t nb = uint32_t((n + SCAN_ITEMS - 1) / SCAN_ITEMS);
+    k_encode_scan_local<<<nb, BLOCK, 0, s>>>(desc, n, wire_off, block_sums);
+    k_encode_scan_blocks<<<1, BLOCK, 0, s>>>(block_sums, nb, block_prefix, wire_off, n);
+    k_encode_finalize<<<(n + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(desc, n, wire_off, block_prefix, tile_first,
+                                                                tiles_cap, wire_cap, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_mask(hipStream_t s, int grid, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
+                              const uint64_t* wire_off, const uint32_t* tile_first, uint8_t* wire,
+                              uint64_t wire_cap)
+{
+    k_encode_mask<<<grid, BLOCK, 0, s>>>(payload, desc, n, wire_off, tile_first, wire, wire_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64_t len, const uint32_t* keys,
+                         uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire)
+{
+    k_fanout<<<grid, BLOCK, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, 1.0 / double(fsize), wire);
+    return hipGetLastError();
+}
+
+hipError_t launch_xor(hipStream_t s, int grid, const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,
+                      uint32_t phase)
+{
+    k_xor<<<grid, BLOCK, 0, s>>>(src, dst, len, key, phase);
+    return hipGetLastError();
+}
+
+} // namespace wsg

@@ -10,9 +10,10 @@
  * entry point returns an int status (WSG_OK = 0, negative on failure).
  *
  * Device ("d_") buffers are caller-owned and must already be resident in HBM.
- * Batch entry points are asynchronous on the given HIP stream (pass NULL for
- * the context's own stream); the caller synchronizes (wsg_sync) before reading
- * outputs.  Data-dependent errors (a frame that overruns the wire, overlapping
+ * Batch entry points are asynchronous on the given HIP stream (NULL = HIP's
+ * default stream, as everywhere in HIP; wsg_stream() returns a non-blocking
+ * stream owned by the context); the caller synchronizes (wsg_sync) before
+ * reading outputs.  Data-dependent errors (a frame that overruns the wire, overlapping
  * frames) are latched in the context and reported by wsg_sync.
  *
  * Thread-safety: one wsg_ctx per host thread.  A ctx is not thread-safe.
@@ -82,7 +83,7 @@ typedef struct wsg_ctx wsg_ctx;
 /* Bind to HIP device `device`, create a non-blocking stream, small scratch.   */
 int wsg_create(int device, wsg_ctx** out);
 int wsg_destroy(wsg_ctx* ctx);
-/* Synchronize the ctx's stream (or `stream` if non-NULL) and return the first
+/* Synchronize `stream` (NULL = default stream) and return the first
  * data-dependent error latched since the last wsg_sync (then clear it).      */
 int wsg_sync(wsg_ctx* ctx, void* stream);
 /* HIP stream owned by the context (a hipStream_t). */

@@ -1,0 +1,293 @@
+"""Parity of the HIP path (through the C-ABI) with the pinned oracle.
+
+Bit-exact for every byte: this is integer/byte work, no tolerance.
+Runs on the MI355X box: `pytest -m gpu`.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from tests import kat
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import cppserver_amd as ca  # noqa: E402
+from cppserver_amd import workloads as wl  # noqa: E402
+from cppserver_amd.layout import RECV_INFO, SEND_DESC, frame_size  # noqa: E402
+
+KAT = kat.load()
+INFO_FIELDS = ["payload_off", "len", "key", "opcode", "fin", "masked", "hdr_len", "b0", "error"]
+
+
+@pytest.fixture(scope="module")
+def codec():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    c = ca.Codec(0)
+    yield c
+    c.close()
+
+
+def dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+def gpu_decode(codec, wire, fs, inplace=False):
+    n = len(fs)
+    w = dev(wire if len(wire) else np.zeros(0, np.uint8))
+    f = dev(np.asarray(fs, dtype=np.uint64).view(np.int64))
+    out = w if inplace else None
+    out, info = codec.decode_batch(w, f, out=out)
+    rc = codec.sync_status()
+    return rc, out.cpu().numpy(), ca.info_to_numpy(info, n)
+
+
+def gpu_encode(codec, payload, desc, cap=None):
+    n = len(desc)
+    if cap is None:
+        cap = int(sum(frame_size(int(d["opcode"]), bool(d["mask"]), int(d["len"]), int(d["status"]))
+                      for d in desc)) if n else 16
+    p = dev(payload if len(payload) else np.zeros(1, np.uint8))
+    d = ca.desc_to_tensor(desc, "cuda")
+    wire, off = codec.encode_batch(p, d, wire_cap=max(cap, 16))
+    rc = codec.sync_status()
+    off = off.cpu().numpy().view(np.uint64)
+    return rc, wire.cpu().numpy()[: int(off[n])] if rc == 0 else None, off
+
+
+def assert_decode_parity(codec, wire, fs, inplace=False):
+    rc_o, out_o, info_o = oracle.decode_batch(wire, fs)
+    rc_g, out_g, info_g = gpu_decode(codec, wire, fs, inplace=inplace)
+    assert rc_g == rc_o
+    assert np.array_equal(out_g, out_o)
+    for f in INFO_FIELDS:
+        assert np.array_equal(info_g[f], info_o[f]), f
+    return out_g, info_g
+
+
+# ---------------------------------------------------------------- golden KATs
+@pytest.mark.parametrize("v", KAT["encode"], ids=lambda v: v["name"])
+def test_encode_kat(codec, v):
+    payload = np.frombuffer(kat.payload_of(v), dtype=np.uint8)
+    desc = np.zeros(1, dtype=SEND_DESC)
+    desc["len"] = len(payload)
+    desc["key"] = kat.key_of(v)
+    desc["status"] = v["status"]
+    desc["opcode"] = v["opcode"]
+    desc["mask"] = v["mask"]
+    rc, wire, _ = gpu_encode(codec, payload, desc)
+    assert rc == 0
+    if "expect" in v:
+        assert wire.tobytes().hex() == v["expect"], v["source"]
+    else:
+        assert wire[: len(v["expect_prefix"]) // 2].tobytes().hex() == v["expect_prefix"]
+        assert len(wire) == v["expect_len"]
+    if v.get("expect_payload_identity"):
+        assert wire[len(wire) - len(payload):].tobytes() == payload.tobytes()
+
+
+def test_decode_kat_frames(codec):
+    """Every whole frame from the decode KATs, decoded as one batch."""
+    frames = [bytes.fromhex(c) for v in KAT["decode"] for c in v["chunks"] if v["name"] != "rfc_fragmented_one_read"]
+    wire = np.frombuffer(b"".join(frames), dtype=np.uint8)
+    fs = np.cumsum([0] + [len(f) for f in frames[:-1]]).astype(np.uint64)
+    out, info = assert_decode_parity(codec, wire, fs)
+    hello = [i for i, f in enumerate(frames) if f.startswith(bytes.fromhex("8185"))][0]
+    p = int(info["payload_off"][hello])
+    assert out[p: p + 5].tobytes() == b"Hello"
+
+
+@pytest.mark.parametrize("v", KAT["roundtrip"], ids=lambda v: v["name"])
+def test_roundtrip_kat(codec, v):
+    payload = np.frombuffer(kat.payload_of(v), dtype=np.uint8)
+    desc = np.zeros(1, dtype=SEND_DESC)
+    desc["len"], desc["key"], desc["status"] = len(payload), kat.key_of(v), v["status"]
+    desc["opcode"], desc["mask"] = v["opcode"], v["mask"]
+    rc, wire, off = gpu_encode(codec, payload, desc)
+    assert rc == 0
+    ref = oracle.Session(kat.key_of(v)).prepare_send(v["opcode"], v["mask"], payload.tobytes(), v["status"])
+    assert wire.tobytes() == ref
+    rc, out, info = gpu_decode(codec, wire, [0])
+    assert rc == 0
+    p, n = int(info["payload_off"][0]), int(info["len"][0])
+    (kind, body, status), = kat.events_of(v)
+    got = out[p: p + n].tobytes()
+    if kind == 2:   # close: status is the first two payload bytes (ws.cpp:435-439)
+        assert (got[0] << 8 | got[1], got[2:]) == (status, body)
+    else:
+        assert got == body
+
+
+# ---------------------------------------------------------------- C2 (headline)
+def test_c2_unmask_full_size_vs_oracle(codec):
+    wire, fs, keys = wl.c2_wire(4096, 65536, seed=21)
+    out, info = assert_decode_parity(codec, wire, fs)
+    assert (info["len"] == 65536).all() and (info["hdr_len"] == 14).all()
+    assert np.array_equal(info["key"], keys)
+
+
+def test_c2_unmask_inplace(codec):
+    wire, fs, _ = wl.c2_wire(512, 65536, seed=22)
+    assert_decode_parity(codec, wire, fs, inplace=True)
+
+
+@pytest.mark.parametrize("size", [0, 1, 2, 3, 15, 16, 17, 125, 126, 127, 4095, 65535, 65536, 65537, 200000])
+def test_uniform_sizes_vs_oracle(codec, size):
+    wire, fs, _ = wl.c2_wire(37, size, seed=size)
+    assert_decode_parity(codec, wire, fs)
+
+
+# ---------------------------------------------------------------- ragged / C3
+def _mixed_desc(rng, n, lo, hi):
+    lens = rng.integers(lo, hi + 1, n)
+    desc, total = wl.ragged_desc(rng, lens)
+    desc["opcode"] = rng.choice([0x81, 0x82, 0x01, 0x02, 0x00, 0x80, 0x88, 0x89, 0x8A, 0xC2, 0x83], n)
+    desc["mask"] = rng.random(n) < 0.6
+    desc["status"] = np.where(rng.random(n) < 0.3, rng.integers(-5, 70000, n), 0)
+    desc["src_off"] += rng.integers(0, 16, n).astype(np.uint64)   # misaligned sources
+    payload = wl.random_bytes(rng, total + 16)
+    return payload, desc
+
+
+@pytest.mark.parametrize("lo,hi,n", [(0, 40, 3000), (0, 300, 2000), (100, 70000, 300), (128, 65536, 4096)])
+def test_encode_mixed_vs_oracle(codec, lo, hi, n):
+    rng = np.random.default_rng(lo * 7 + hi + n)
+    payload, desc = _mixed_desc(rng, n, lo, hi)
+    wire_o, off_o = oracle.encode_batch(payload, desc)
+    rc, wire_g, off_g = gpu_encode(codec, payload, desc)
+    assert rc == 0
+    assert np.array_equal(off_g, off_o)
+    assert np.array_equal(wire_g, wire_o)
+    # and the GPU decode of that wire matches the oracle decode
+    assert_decode_parity(codec, wire_o, off_o[:-1])
+
+
+def test_c3_roundtrip_full_size(codec):
+    """C3 at BASELINE size (65536 frames, 128 B-64 KiB): encode -> decode on the
+    GPU returns every payload byte (size-independent property), plus oracle
+    parity on the first 2048 frames."""
+    payload, desc = wl.c3_batch(65536, 128, 65536, seed=31)
+    n = len(desc)
+    p = dev(payload)
+    d = ca.desc_to_tensor(desc, "cuda")
+    cap = int(sum(frame_size(0x82, True, int(x)) for x in desc["len"]))
+    wire, off = codec.encode_batch(p, d, wire_cap=cap)
+    out, info = codec.decode_batch(wire[:cap], off[:-1])
+    codec.sync()
+    info = ca.info_to_numpy(info, n)
+    offs = off.cpu().numpy().view(np.uint64)
+    assert int(offs[-1]) == cap
+    assert np.array_equal(info["len"], desc["len"])
+    # drop the header bytes: what remains must be the payload arena, in order
+    hdr = info["hdr_len"].astype(np.int64)
+    starts = offs[:-1].astype(np.int64)
+    excl = np.concatenate([[0], np.cumsum(hdr)[:-1]])
+    hdr_idx = np.repeat(starts, hdr) + (np.arange(int(hdr.sum())) - np.repeat(excl, hdr))
+    keep = torch.ones(cap, dtype=torch.bool, device="cuda")
+    keep[torch.from_numpy(hdr_idx).cuda()] = False
+    pos, step = 0, 1 << 28          # chunked: torch masked_select overflows past 2**31 elements
+    for a in range(0, cap, step):
+        sel = out[a: min(cap, a + step)][keep[a: min(cap, a + step)]]
+        assert torch.equal(sel, p[pos: pos + sel.numel()])
+        pos += sel.numel()
+    assert pos == len(payload)
+    sub = 2048
+    wire_o, off_o = oracle.encode_batch(payload, desc[:sub])
+    assert np.array_equal(wire[: int(off_o[sub])].cpu().numpy(), wire_o)
+
+
+# ---------------------------------------------------------------- C4 fan-out
+def test_c4_fanout_vs_oracle(codec):
+    payload, keys = wl.c4_fanout(4096, 10000, seed=41)
+    ref = oracle.fanout_encode(payload, keys, 0x82, True)
+    wire = codec.fanout(dev(payload), dev(keys.view(np.int32)), 0x82, True)
+    codec.sync()
+    assert np.array_equal(wire.cpu().numpy()[: len(ref)], ref)
+
+
+@pytest.mark.parametrize("length,k,opcode,mask", [(0, 5, 0x88, True), (1, 33, 0x89, False), (125, 100, 0x81, True),
+                                                 (126, 100, 0x82, False), (5000, 77, 0x8A, True),
+                                                 (65536, 9, 0x82, True)])
+def test_fanout_shapes(codec, length, k, opcode, mask):
+    payload, keys = wl.c4_fanout(length, k, seed=length + k)
+    ref = oracle.fanout_encode(payload, keys, opcode, mask)
+    wire = codec.fanout(dev(payload if length else np.zeros(1, np.uint8)), dev(keys.view(np.int32)), opcode, mask,
+                        length=length)
+    codec.sync()
+    assert np.array_equal(wire.cpu().numpy()[: len(ref)], ref)
+
+
+# ---------------------------------------------------------------- edge cases
+def test_empty_batches(codec):
+    rc, out, info = gpu_decode(codec, np.zeros(32, np.uint8), [])
+    assert rc == 0 and np.array_equal(out, np.zeros(32, np.uint8))
+    rc, wire, off = gpu_encode(codec, np.zeros(1, np.uint8), np.zeros(0, dtype=SEND_DESC))
+    assert rc == 0 and off[0] == 0
+
+
+def test_decode_errors_match_oracle(codec):
+    frame = bytes([0x82, 0x05, 1, 2, 3, 4, 5])
+    masked = oracle.Session(0x01020304).prepare_send(0x82, True, bytes(range(40)))
+    wire = np.frombuffer(masked + frame + frame, dtype=np.uint8)
+    n1 = len(masked)
+    for fs, cut in [([0, n1, n1 + 7], 1), ([0, n1, n1 + 3], 0), ([0, 5], 0), ([0, n1, n1 + 7], 10)]:
+        w = wire[: len(wire) - cut]
+        rc_o, out_o, info_o = oracle.decode_batch(w, fs)
+        rc_g, out_g, info_g = gpu_decode(codec, w, fs)
+        assert rc_o != 0 and rc_g == rc_o
+        assert np.array_equal(info_g["error"], info_o["error"])
+        ok = info_o["error"] == 0
+        for f in INFO_FIELDS:
+            assert np.array_equal(info_g[f][ok], info_o[f][ok]), f
+        assert np.array_equal(out_g, out_o)
+
+
+def test_misaligned_buffers_rejected(codec):
+    w = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    f = torch.zeros(1, dtype=torch.int64, device="cuda")
+    with pytest.raises(ca.WSGError) as e:
+        codec.decode_batch(w[1:], f)
+    assert e.value.code == ca.WSG_EINVAL
+
+
+def test_encode_capacity_error(codec):
+    payload = np.zeros(1000, np.uint8)
+    desc = np.zeros(4, dtype=SEND_DESC)
+    desc["len"] = 250
+    desc["opcode"] = 0x82
+    rc, _, _ = gpu_encode(codec, payload, desc, cap=500)
+    assert rc == ca.WSG_ENOMEM
+
+
+# ---------------------------------------------------------------- host-staged
+@pytest.mark.parametrize("n,key,phase", [(1, 0xDEADBEEF, 0), (15, 1, 3), (4097, 0xA1B2C3D4, 2), (1 << 20, 7, 1)])
+def test_xor_host(codec, n, key, phase):
+    data = wl.random_bytes(np.random.default_rng(n), n)
+    kb = np.frombuffer(int(key).to_bytes(4, "little"), np.uint8)
+    exp = data ^ kb[(np.arange(n) + phase) % 4]
+    assert codec.xor_host(data.tobytes(), key, phase) == exp.tobytes()
+
+
+def test_decode_batch_host(codec):
+    wire, fs, _ = wl.c2_wire(64, 5000, seed=9)
+    rc, out, info = codec.decode_batch_host(wire, fs)
+    rc_o, out_o, info_o = oracle.decode_batch(wire, fs)
+    assert rc == rc_o == 0
+    assert np.array_equal(out, out_o)
+    for f in INFO_FIELDS:
+        assert np.array_equal(info[f], info_o[f])
+
+
+def test_timing_hook_counts_launches(codec):
+    wire, fs, _ = wl.c2_wire(64, 65536, seed=10)
+    w, f = dev(wire), dev(fs.view(np.int64))
+    codec.timing(True)
+    for _ in range(3):
+        codec.decode_batch(w, f)
+    ms, launches = codec.timing_read()
+    codec.timing(False)
+    codec.sync()
+    assert launches == 3 and ms > 0

@@ -1,0 +1,115 @@
+// membench.hip — streaming read+write ceiling on gfx950 for the access shape
+// of the unmask kernel (16 B per lane, coalesced, out-of-place and in-place).
+// Diagnostic tool only (not part of the product): tells which block size,
+// steps-per-lane and cache policy reach the HBM roof for a copy-with-XOR.
+//
+//   hipcc --offload-arch=gfx950 -O3 -o membench membench.hip && ./membench [MiB]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                     \
+    do {                                                                          \
+        hipError_t e = (x);                                                       \
+        if (e != hipSuccess) {                                                    \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+            exit(1);                                                              \
+        }                                                                         \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int BLOCK, int U, int NT>
+__global__ __launch_bounds__(BLOCK) void k_stream(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                  uint64_t n16, uint32_t key)
+{
+    const uint64_t per_tile = uint64_t(BLOCK) * U;
+    const uint64_t tiles = n16 / per_tile;
+    for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = t * per_tile + uint64_t(u) * BLOCK + threadIdx.x;
+            if (NT & 1)
+                v[u] = __builtin_nontemporal_load(src + i);
+            else
+                v[u] = src[i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = t * per_tile + uint64_t(u) * BLOCK + threadIdx.x;
+            u32x4 w = v[u] ^ key;
+            if (NT & 2)
+                __builtin_nontemporal_store(w, dst + i);
+            else
+                dst[i] = w;
+        }
+    }
+}
+
+template <int BLOCK, int U, int NT>
+void run(const char* name, const u32x4* src, u32x4* dst, uint64_t n16, int cus, int bpc)
+{
+    const uint64_t tiles = n16 / (uint64_t(BLOCK) * U);
+    const int grid = int(std::min<uint64_t>(tiles, uint64_t(cus) * bpc));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i)
+        k_stream<BLOCK, U, NT><<<grid, BLOCK>>>(src, dst, n16, 0x12345678u);
+    const int reps = 20;
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i)
+        k_stream<BLOCK, U, NT><<<grid, BLOCK>>>(src, dst, n16, 0x12345678u);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    ms /= reps;
+    const double gbs = 2.0 * n16 * 16 / (ms * 1e-3) / 1e9;
+    printf("%-34s block=%4d U=%2d nt=%d bpc=%2d grid=%6d  %8.1f us  %7.1f GB/s\n", name, BLOCK, U, NT, bpc, grid,
+           ms * 1e3, gbs);
+    CK(hipEventDestroy(a));
+    CK(hipEventDestroy(b));
+}
+
+int main(int argc, char** argv)
+{
+    const uint64_t mib = argc > 1 ? strtoull(argv[1], 0, 10) : 256;
+    const uint64_t bytes = mib << 20;
+    const uint64_t n16 = bytes / 16;
+    hipDeviceProp_t p;
+    CK(hipGetDeviceProperties(&p, 0));
+    const int cus = p.multiProcessorCount;
+    printf("device %s CUs=%d bytes=%llu MiB\n", p.gcnArchName, cus, (unsigned long long)mib);
+    u32x4 *src, *dst;
+    CK(hipMalloc(&src, bytes));
+    CK(hipMalloc(&dst, bytes));
+    CK(hipMemset(src, 1, bytes));
+    CK(hipMemset(dst, 0, bytes));
+    for (int bpc : {4, 8, 16}) {
+        run<256, 4, 0>("oop", src, dst, n16, cus, bpc);
+        run<256, 4, 3>("oop", src, dst, n16, cus, bpc);
+    }
+    run<256, 8, 0>("oop", src, dst, n16, cus, 8);
+    run<256, 8, 3>("oop", src, dst, n16, cus, 8);
+    run<256, 8, 2>("oop", src, dst, n16, cus, 8);
+    run<256, 8, 1>("oop", src, dst, n16, cus, 8);
+    run<256, 16, 0>("oop", src, dst, n16, cus, 4);
+    run<256, 16, 3>("oop", src, dst, n16, cus, 4);
+    run<512, 4, 0>("oop", src, dst, n16, cus, 4);
+    run<512, 8, 3>("oop", src, dst, n16, cus, 4);
+    run<1024, 4, 0>("oop", src, dst, n16, cus, 2);
+    run<1024, 4, 3>("oop", src, dst, n16, cus, 2);
+    run<256, 4, 0>("oop grid=all tiles", src, dst, n16, cus, 1 << 20);
+    run<256, 4, 3>("oop grid=all tiles", src, dst, n16, cus, 1 << 20);
+    run<256, 8, 3>("oop grid=all tiles", src, dst, n16, cus, 1 << 20);
+    run<256, 4, 0>("inplace", src, src, n16, cus, 8);
+    run<256, 4, 3>("inplace", src, src, n16, cus, 8);
+    run<256, 8, 3>("inplace", src, src, n16, cus, 8);
+    CK(hipFree(src));
+    CK(hipFree(dst));
+    return 0;
+}
