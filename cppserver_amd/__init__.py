@@ -61,6 +61,13 @@ def lib():
         "wsg_frame_size": (u64, [ctypes.c_uint8, ci, u64, i32]),
         "wsg_header_pack": (ci, [ctypes.c_uint8, ci, u64, i32, u32, vp]),
         "wsg_header_unpack": (ci, [vp, u64, vp]),
+        "wsg_session_create": (ci, [vp, ctypes.POINTER(vp)]),
+        "wsg_session_destroy": (ci, [vp]),
+        "wsg_session_set_send_key": (ci, [vp, u32]),
+        "wsg_session_prepare_send": (ci, [vp, ctypes.c_uint8, ci, vp, sz, i32, vp, sz, ctypes.POINTER(sz)]),
+        "wsg_session_prepare_receive": (ci, [vp, vp, sz, vp, vp]),
+        "wsg_session_required": (sz, [vp]),
+        "wsg_session_clear": (ci, [vp]),
         "wsg_timing_enable": (ci, [vp, ci]),
         "wsg_timing_read": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ci]),
     }
@@ -213,6 +220,65 @@ class Codec:
         _check(self._L.wsg_timing_read(self._ctx, ctypes.byref(ms), ctypes.byref(n), 1 if reset else 0),
                "wsg_timing_read")
         return ms.value, n.value
+
+
+RECEIVE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t,
+                              ctypes.c_int)
+
+
+class Session:
+    """One connection's codec state through the C-ABI (wsg_session_*): the
+    reference WebSocket mix-in with its payload XOR on the GPU."""
+
+    def __init__(self, codec, send_key=0):
+        self._L = lib()
+        self._codec = codec          # keeps the ctx alive
+        s = ctypes.c_void_p()
+        _check(self._L.wsg_session_create(codec._ctx, ctypes.byref(s)), "wsg_session_create")
+        self._s = s
+        self.set_send_key(send_key)
+        self._events = []
+
+        def _cb(user, kind, data, size, status):
+            self._events.append((kind, ctypes.string_at(data, size) if size else b"", status))
+
+        self._cb = RECEIVE_CB(_cb)
+
+    def close(self):
+        if getattr(self, "_s", None):
+            self._L.wsg_session_destroy(self._s)
+            self._s = None
+
+    __del__ = close
+
+    def set_send_key(self, key):
+        _check(self._L.wsg_session_set_send_key(self._s, key), "wsg_session_set_send_key")
+
+    def prepare_send(self, opcode, mask, payload=b"", status=0):
+        buf = bytes(payload)
+        cap = frame_size(opcode, mask, len(buf), status)
+        out = ctypes.create_string_buffer(max(cap, 1))
+        n = ctypes.c_size_t()
+        _check(self._L.wsg_session_prepare_send(self._s, opcode, 1 if mask else 0, buf, len(buf), status, out, cap,
+                                                ctypes.byref(n)), "wsg_session_prepare_send")
+        return out.raw[: n.value]
+
+    def prepare_receive(self, data):
+        buf = bytes(data)
+        _check(self._L.wsg_session_prepare_receive(self._s, buf if buf else None, len(buf), self._cb, None),
+               "wsg_session_prepare_receive")
+
+    def events(self, clear=True):
+        ev = list(self._events)
+        if clear:
+            self._events.clear()
+        return ev
+
+    def required(self):
+        return self._L.wsg_session_required(self._s)
+
+    def clear(self):
+        _check(self._L.wsg_session_clear(self._s), "wsg_session_clear")
 
 
 def info_to_numpy(info_tensor, n):

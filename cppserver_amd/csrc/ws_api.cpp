@@ -1,0 +1,259 @@
+// ws_api.cpp — WSClient / WSSession / WSServer over a Transport.
+//
+// Send* = lock _ws_send_lock, PrepareSendFrame (payload masked on the GPU),
+// hand the frame to the transport (reference ws_client.h:53-90,
+// ws_session.h:46-83).  onReceived routes post-upgrade bytes to
+// PrepareReceiveFrame (ws_client.cpp:76-87, ws_session.cpp:40-51).
+// Multicast encodes once and queues the same bytes on every handshaked
+// session (ws_server.cpp:36-64).
+#include "server/ws/ws_client.h"
+#include "server/ws/ws_server.h"
+#include "server/ws/ws_session.h"
+
+#include <algorithm>
+
+namespace CppServer {
+namespace WS {
+
+namespace {
+
+// Synchronous framing loop shared by client and session Receive*
+// (reference ws_client.cpp:139-157).  The reference then copies from
+// final_buffer + header_size (ws_client.cpp:155), skipping the
+// first header_size payload bytes; this build returns the whole message.
+template <class Required, class Prepare, class Recv>
+bool receive_message(std::vector<uint8_t>& out, Required required, Prepare prepare, Recv recv,
+                     const std::vector<uint8_t>& final_buf, const bool& frame_received, const bool& final_received)
+{
+    std::vector<uint8_t> cache;
+    while (!final_received) {
+        while (!frame_received) {
+            const size_t want = required();
+            cache.resize(want);
+            if (recv(cache.data(), want) != want)
+                return false;
+            prepare(cache.data(), want);
+        }
+        if (!final_received)
+            prepare(nullptr, 0);
+    }
+    out.assign(final_buf.begin(), final_buf.end());
+    prepare(nullptr, 0);
+    return true;
+}
+
+} // namespace
+
+// ---------------------------------------------------------------- WSClient
+
+bool WSClient::Connect()
+{
+    if (!_transport.IsConnected())
+        return false;
+    ClearWSBuffers();
+    InitWSNonce();
+    Handshaked(true);
+    onWSConnected();
+    return true;
+}
+
+bool WSClient::Disconnect()
+{
+    const bool ok = _transport.Disconnect();
+    onDisconnected();
+    return ok;
+}
+
+void WSClient::onDisconnected()
+{
+    if (_ws_handshaked) {
+        _ws_handshaked = false;
+        onWSDisconnected();
+    }
+    ClearWSBuffers();
+    InitWSNonce();
+}
+
+void WSClient::onReceived(const void* buffer, size_t size)
+{
+    if (_ws_handshaked)
+        PrepareReceiveFrame(buffer, size);
+}
+
+size_t WSClient::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status)
+{
+    std::scoped_lock locker(_ws_send_lock);
+    PrepareSendFrame(opcode, true, buffer, size, status);
+    return _transport.Send(_ws_send_buffer.data(), _ws_send_buffer.size());
+}
+
+bool WSClient::SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status)
+{
+    std::scoped_lock locker(_ws_send_lock);
+    PrepareSendFrame(opcode, true, buffer, size, status);
+    return _transport.SendAsync(_ws_send_buffer.data(), _ws_send_buffer.size());
+}
+
+bool WSClient::ReceiveMessage(std::vector<uint8_t>& out)
+{
+    if (!_ws_handshaked)
+        return false;
+    return receive_message(
+        out, [this]() { return RequiredReceiveFrameSize(); },
+        [this](const void* b, size_t n) { PrepareReceiveFrame(b, n); },
+        [this](void* b, size_t n) { return _transport.Receive(b, n); }, _ws_receive_final_buffer,
+        _ws_frame_received, _ws_final_received);
+}
+
+std::string WSClient::ReceiveText()
+{
+    std::vector<uint8_t> msg;
+    if (!ReceiveMessage(msg))
+        return std::string();
+    return std::string(msg.begin(), msg.end());
+}
+
+std::vector<uint8_t> WSClient::ReceiveBinary()
+{
+    std::vector<uint8_t> msg;
+    ReceiveMessage(msg);
+    return msg;
+}
+
+// ---------------------------------------------------------------- WSSession
+
+bool WSSession::Connect()
+{
+    if (!_transport.IsConnected())
+        return false;
+    ClearWSBuffers();
+    Handshaked(false);
+    onWSConnected();
+    return true;
+}
+
+bool WSSession::Disconnect()
+{
+    const bool ok = _transport.Disconnect();
+    onDisconnected();
+    return ok;
+}
+
+void WSSession::onDisconnected()
+{
+    if (_ws_handshaked) {
+        _ws_handshaked = false;
+        onWSDisconnected();
+    }
+    ClearWSBuffers();
+    InitWSNonce();
+}
+
+void WSSession::onReceived(const void* buffer, size_t size)
+{
+    if (_ws_handshaked)
+        PrepareReceiveFrame(buffer, size);
+}
+
+size_t WSSession::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status)
+{
+    std::scoped_lock locker(_ws_send_lock);
+    PrepareSendFrame(opcode, false, buffer, size, status);
+    return _transport.Send(_ws_send_buffer.data(), _ws_send_buffer.size());
+}
+
+bool WSSession::SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status)
+{
+    std::scoped_lock locker(_ws_send_lock);
+    PrepareSendFrame(opcode, false, buffer, size, status);
+    return _transport.SendAsync(_ws_send_buffer.data(), _ws_send_buffer.size());
+}
+
+bool WSSession::ReceiveMessage(std::vector<uint8_t>& out)
+{
+    if (!_ws_handshaked)
+        return false;
+    return receive_message(
+        out, [this]() { return RequiredReceiveFrameSize(); },
+        [this](const void* b, size_t n) { PrepareReceiveFrame(b, n); },
+        [this](void* b, size_t n) { return _transport.Receive(b, n); }, _ws_receive_final_buffer,
+        _ws_frame_received, _ws_final_received);
+}
+
+std::string WSSession::ReceiveText()
+{
+    std::vector<uint8_t> msg;
+    if (!ReceiveMessage(msg))
+        return std::string();
+    return std::string(msg.begin(), msg.end());
+}
+
+std::vector<uint8_t> WSSession::ReceiveBinary()
+{
+    std::vector<uint8_t> msg;
+    ReceiveMessage(msg);
+    return msg;
+}
+
+// ---------------------------------------------------------------- WSServer
+
+void WSServer::AddSession(const std::shared_ptr<WSSession>& session)
+{
+    std::unique_lock<std::shared_mutex> locker(_sessions_lock);
+    _sessions.push_back(session);
+}
+
+void WSServer::RemoveSession(const std::shared_ptr<WSSession>& session)
+{
+    std::unique_lock<std::shared_mutex> locker(_sessions_lock);
+    _sessions.erase(std::remove(_sessions.begin(), _sessions.end(), session), _sessions.end());
+}
+
+size_t WSServer::sessions() const
+{
+    std::shared_lock<std::shared_mutex> locker(_sessions_lock);
+    return _sessions.size();
+}
+
+bool WSServer::Multicast(const void* buffer, size_t size)
+{
+    if (size == 0)
+        return true;
+    if (buffer == nullptr)
+        return false;
+    std::shared_lock<std::shared_mutex> locker(_sessions_lock);
+    for (auto& session : _sessions) {
+        std::scoped_lock ws_locker(session->_ws_send_lock);
+        if (session->_ws_handshaked)
+            session->_transport.SendAsync(buffer, size);
+    }
+    return true;
+}
+
+size_t WSServer::MulticastFrame(uint8_t opcode, const void* buffer, size_t size)
+{
+    std::scoped_lock locker(_ws_send_lock);
+    PrepareSendFrame(opcode, false, buffer, size);
+    return Multicast(_ws_send_buffer.data(), _ws_send_buffer.size());
+}
+
+bool WSServer::CloseAll(int status, const void* buffer, size_t size)
+{
+    std::vector<std::shared_ptr<WSSession>> all;
+    {
+        std::scoped_lock locker(_ws_send_lock);
+        PrepareSendFrame(WS_FIN | WS_CLOSE, false, buffer, size, status);
+        if (!Multicast(_ws_send_buffer.data(), _ws_send_buffer.size()))
+            return false;
+    }
+    {
+        std::shared_lock<std::shared_mutex> locker(_sessions_lock);
+        all = _sessions;
+    }
+    for (auto& s : all)
+        s->Disconnect();
+    return true;
+}
+
+} // namespace WS
+} // namespace CppServer

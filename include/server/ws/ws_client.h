@@ -1,0 +1,91 @@
+/*
+ * server/ws/ws_client.h — WebSocket client over a Transport.
+ *
+ * Same Send, Close and Receive surface as the reference WSClient
+ * (include/server/ws/ws_client.h:39-96): every send locks _ws_send_lock,
+ * encodes with mask = true and the connection's random key, and hands the
+ * frame to the transport.  Timeout overloads (CppCommon::Timespan) are not
+ * carried over: timeouts belong to the transport.
+ */
+#ifndef CPPSERVER_AMD_WS_CLIENT_H
+#define CPPSERVER_AMD_WS_CLIENT_H
+
+#include "server/ws/ws.h"
+#include "server/ws/ws_transport.h"
+
+namespace CppServer {
+namespace WS {
+
+class WSClient : protected WebSocket
+{
+public:
+    explicit WSClient(Transport& transport, wsg_ctx* codec = nullptr) : WebSocket(codec), _transport(transport) {}
+    virtual ~WSClient() = default;
+
+    //! Complete the connection: clear buffers, upgrade (random client key), onWSConnected
+    virtual bool Connect();
+    virtual bool Disconnect();
+    bool IsConnected() const { return _transport.IsConnected() && _ws_handshaked; }
+
+    virtual bool Close() { return Close(0, nullptr, 0); }
+    virtual bool Close(int status) { return Close(status, nullptr, 0); }
+    virtual bool Close(int status, const void* buffer, size_t size) { SendClose(status, buffer, size); return Disconnect(); }
+    virtual bool Close(int status, std::string_view text) { SendClose(status, text); return Disconnect(); }
+    virtual bool CloseAsync() { return CloseAsync(0, nullptr, 0); }
+    virtual bool CloseAsync(int status) { return CloseAsync(status, nullptr, 0); }
+    virtual bool CloseAsync(int status, const void* buffer, size_t size) { SendCloseAsync(status, buffer, size); return Disconnect(); }
+    virtual bool CloseAsync(int status, std::string_view text) { SendCloseAsync(status, text); return Disconnect(); }
+
+    size_t SendText(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_TEXT, buffer, size); }
+    size_t SendText(std::string_view text) { return SendFrame(WS_FIN | WS_TEXT, text.data(), text.size()); }
+    bool SendTextAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_TEXT, buffer, size); }
+    bool SendTextAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_TEXT, text.data(), text.size()); }
+
+    size_t SendBinary(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_BINARY, buffer, size); }
+    size_t SendBinary(std::string_view text) { return SendFrame(WS_FIN | WS_BINARY, text.data(), text.size()); }
+    bool SendBinaryAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_BINARY, buffer, size); }
+    bool SendBinaryAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_BINARY, text.data(), text.size()); }
+
+    size_t SendClose(int status, const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_CLOSE, buffer, size, status); }
+    size_t SendClose(int status, std::string_view text) { return SendFrame(WS_FIN | WS_CLOSE, text.data(), text.size(), status); }
+    bool SendCloseAsync(int status, const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_CLOSE, buffer, size, status); }
+    bool SendCloseAsync(int status, std::string_view text) { return SendFrameAsync(WS_FIN | WS_CLOSE, text.data(), text.size(), status); }
+
+    size_t SendPing(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_PING, buffer, size); }
+    size_t SendPing(std::string_view text) { return SendFrame(WS_FIN | WS_PING, text.data(), text.size()); }
+    bool SendPingAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_PING, buffer, size); }
+    bool SendPingAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_PING, text.data(), text.size()); }
+
+    size_t SendPong(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_PONG, buffer, size); }
+    size_t SendPong(std::string_view text) { return SendFrame(WS_FIN | WS_PONG, text.data(), text.size()); }
+    bool SendPongAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_PONG, buffer, size); }
+    bool SendPongAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_PONG, text.data(), text.size()); }
+
+    //! Synchronous receive of one message (reference ws_client.cpp:129-251).
+    std::string ReceiveText();
+    std::vector<uint8_t> ReceiveBinary();
+
+    //! Bytes read by the transport (the reference's TCPClient::onReceived override)
+    void onReceived(const void* buffer, size_t size);
+    //! Transport closed (reference ws_client.cpp:56-74)
+    void onDisconnected();
+
+    using WebSocket::send_key;
+
+protected:
+    //! Reply to close with close, to ping with pong (reference ws_client.h:107-109)
+    void onWSClose(const void* buffer, size_t size, int status = 1000) override { CloseAsync(); }
+    void onWSPing(const void* buffer, size_t size) override { SendPongAsync(buffer, size); }
+
+    Transport& _transport;
+
+private:
+    size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0);
+    bool SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status = 0);
+    bool ReceiveMessage(std::vector<uint8_t>& out);
+};
+
+} // namespace WS
+} // namespace CppServer
+
+#endif // CPPSERVER_AMD_WS_CLIENT_H

@@ -1,0 +1,57 @@
+/*
+ * server/ws/ws_server.h — WebSocket server: the session registry and the
+ * multicast / close-all fan-out of the reference WSServer
+ * (include/server/ws/ws_server.h:41-59, source/server/ws/ws_server.cpp:14-64).
+ *
+ * Multicast* encodes ONE unmasked frame with the server key 0 and queues the
+ * same bytes on every handshaked session, each under its own send lock.
+ */
+#ifndef CPPSERVER_AMD_WS_SERVER_H
+#define CPPSERVER_AMD_WS_SERVER_H
+
+#include "server/ws/ws_session.h"
+
+#include <memory>
+#include <shared_mutex>
+#include <vector>
+
+namespace CppServer {
+namespace WS {
+
+class WSServer : protected WebSocket
+{
+public:
+    explicit WSServer(wsg_ctx* codec = nullptr) : WebSocket(codec) {}
+    virtual ~WSServer() = default;
+
+    //! Register / unregister a connected session (the reference's TCPServer session map)
+    void AddSession(const std::shared_ptr<WSSession>& session);
+    void RemoveSession(const std::shared_ptr<WSSession>& session);
+    size_t sessions() const;
+
+    virtual bool CloseAll() { return CloseAll(0, nullptr, 0); }
+    virtual bool CloseAll(int status) { return CloseAll(status, nullptr, 0); }
+    virtual bool CloseAll(int status, const void* buffer, size_t size);
+    virtual bool CloseAll(int status, std::string_view text) { return CloseAll(status, text.data(), text.size()); }
+
+    //! Queue the same bytes on every handshaked session
+    bool Multicast(const void* buffer, size_t size);
+
+    size_t MulticastText(const void* buffer, size_t size) { return MulticastFrame(WS_FIN | WS_TEXT, buffer, size); }
+    size_t MulticastText(std::string_view text) { return MulticastFrame(WS_FIN | WS_TEXT, text.data(), text.size()); }
+    size_t MulticastBinary(const void* buffer, size_t size) { return MulticastFrame(WS_FIN | WS_BINARY, buffer, size); }
+    size_t MulticastBinary(std::string_view text) { return MulticastFrame(WS_FIN | WS_BINARY, text.data(), text.size()); }
+    size_t MulticastPing(const void* buffer, size_t size) { return MulticastFrame(WS_FIN | WS_PING, buffer, size); }
+    size_t MulticastPing(std::string_view text) { return MulticastFrame(WS_FIN | WS_PING, text.data(), text.size()); }
+
+private:
+    size_t MulticastFrame(uint8_t opcode, const void* buffer, size_t size);
+
+    mutable std::shared_mutex _sessions_lock;
+    std::vector<std::shared_ptr<WSSession>> _sessions;
+};
+
+} // namespace WS
+} // namespace CppServer
+
+#endif // CPPSERVER_AMD_WS_SERVER_H

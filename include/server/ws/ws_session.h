@@ -1,0 +1,84 @@
+/*
+ * server/ws/ws_session.h — server-side WebSocket session over a Transport.
+ *
+ * Same surface as the reference WSSession (include/server/ws/ws_session.h:40-89):
+ * sends are unmasked (mask = false) with the server key 0 (ws.cpp:206).
+ */
+#ifndef CPPSERVER_AMD_WS_SESSION_H
+#define CPPSERVER_AMD_WS_SESSION_H
+
+#include "server/ws/ws.h"
+#include "server/ws/ws_transport.h"
+
+namespace CppServer {
+namespace WS {
+
+class WSServer;
+
+class WSSession : protected WebSocket
+{
+    friend class WSServer;
+
+public:
+    explicit WSSession(Transport& transport, wsg_ctx* codec = nullptr) : WebSocket(codec), _transport(transport) {}
+    virtual ~WSSession() = default;
+
+    //! Upgrade accepted: clear buffers, key 0, onWSConnected
+    virtual bool Connect();
+    virtual bool Disconnect();
+    bool IsConnected() const { return _transport.IsConnected() && _ws_handshaked; }
+
+    virtual bool Close() { return Close(0, nullptr, 0); }
+    virtual bool Close(int status) { return Close(status, nullptr, 0); }
+    virtual bool Close(int status, const void* buffer, size_t size) { SendCloseAsync(status, buffer, size); return Disconnect(); }
+    virtual bool Close(int status, std::string_view text) { SendCloseAsync(status, text); return Disconnect(); }
+
+    size_t SendText(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_TEXT, buffer, size); }
+    size_t SendText(std::string_view text) { return SendFrame(WS_FIN | WS_TEXT, text.data(), text.size()); }
+    bool SendTextAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_TEXT, buffer, size); }
+    bool SendTextAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_TEXT, text.data(), text.size()); }
+
+    size_t SendBinary(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_BINARY, buffer, size); }
+    size_t SendBinary(std::string_view text) { return SendFrame(WS_FIN | WS_BINARY, text.data(), text.size()); }
+    bool SendBinaryAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_BINARY, buffer, size); }
+    bool SendBinaryAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_BINARY, text.data(), text.size()); }
+
+    size_t SendClose(int status, const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_CLOSE, buffer, size, status); }
+    size_t SendClose(int status, std::string_view text) { return SendFrame(WS_FIN | WS_CLOSE, text.data(), text.size(), status); }
+    bool SendCloseAsync(int status, const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_CLOSE, buffer, size, status); }
+    bool SendCloseAsync(int status, std::string_view text) { return SendFrameAsync(WS_FIN | WS_CLOSE, text.data(), text.size(), status); }
+
+    size_t SendPing(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_PING, buffer, size); }
+    size_t SendPing(std::string_view text) { return SendFrame(WS_FIN | WS_PING, text.data(), text.size()); }
+    bool SendPingAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_PING, buffer, size); }
+    bool SendPingAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_PING, text.data(), text.size()); }
+
+    size_t SendPong(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_PONG, buffer, size); }
+    size_t SendPong(std::string_view text) { return SendFrame(WS_FIN | WS_PONG, text.data(), text.size()); }
+    bool SendPongAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_PONG, buffer, size); }
+    bool SendPongAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_PONG, text.data(), text.size()); }
+
+    std::string ReceiveText();
+    std::vector<uint8_t> ReceiveBinary();
+
+    //! Bytes read by the transport (reference ws_session.cpp:40-51)
+    void onReceived(const void* buffer, size_t size);
+    //! Transport closed (reference ws_session.cpp:20-38)
+    void onDisconnected();
+
+protected:
+    void onWSClose(const void* buffer, size_t size, int status = 1000) override { Close(); }
+    void onWSPing(const void* buffer, size_t size) override { SendPongAsync(buffer, size); }
+
+    Transport& _transport;
+
+private:
+    size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0);
+    bool SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status = 0);
+    bool ReceiveMessage(std::vector<uint8_t>& out);
+};
+
+} // namespace WS
+} // namespace CppServer
+
+#endif // CPPSERVER_AMD_WS_SESSION_H
