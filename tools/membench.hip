@@ -8,6 +8,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                     \
@@ -89,6 +90,14 @@ int main(int argc, char** argv)
     CK(hipMalloc(&dst, bytes));
     CK(hipMemset(src, 1, bytes));
     CK(hipMemset(dst, 0, bytes));
+    if (argc > 2 && std::string(argv[2]) == "calib") {
+        // PMC calibration: known bytes (read n16*16, write n16*16 per launch)
+        run<256, 4, 0>("calib plain", src, dst, n16, cus, 8);
+        run<256, 4, 3>("calib nt", src, dst, n16, cus, 8);
+        CK(hipFree(src));
+        CK(hipFree(dst));
+        return 0;
+    }
     for (int bpc : {4, 8, 16}) {
         run<256, 4, 0>("oop", src, dst, n16, cus, bpc);
         run<256, 4, 3>("oop", src, dst, n16, cus, bpc);
