@@ -33,17 +33,21 @@ class WSGError(RuntimeError):
         super().__init__("%s failed: %s (%d)" % (what or "wsg", msg, code))
 
 
-def lib():
-    """Load the HIP codec library; raise loudly if it was not built."""
+def lib(path=None):
+    """Load the HIP codec library; raise loudly if it was not built.
+
+    `path` loads another build of the same ABI (A/B tuning); default is the
+    in-tree library."""
     global _lib
-    if _lib is not None:
+    if path is None and _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    p = path or LIB_PATH
+    if not os.path.exists(p):
         raise ImportError(
             "cppserver_amd: native library %s is missing; run `python -c 'import __graft_entry__ as g; g.build()'` "
-            "(or `make -C cppserver_amd`). There is no CPU fallback." % LIB_PATH
+            "(or `make -C cppserver_amd`). There is no CPU fallback." % p
         )
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(p)
     vp, u32, u64, i32, sz, ci = (ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32,
                                  ctypes.c_size_t, ctypes.c_int)
     sig = {
@@ -75,7 +79,8 @@ def lib():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = L
+    if path is None:
+        _lib = L
     return L
 
 
@@ -116,14 +121,14 @@ class Codec:
     :meth:`sync` before reading results on the host.
     """
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, lib_path=None):
         import torch
 
         self._torch = torch
+        self._L = lib(lib_path)
         if not torch.cuda.is_available():
             raise WSGError(WSG_EHIP, "Codec: no HIP device visible")
         self.device = torch.device("cuda", device)
-        self._L = lib()
         ctx = ctypes.c_void_p()
         _check(self._L.wsg_create(device, ctypes.byref(ctx)), "wsg_create")
         self._ctx = ctx
@@ -212,8 +217,9 @@ class Codec:
         return rc, out[: len(wire)], info[: len(fs)]
 
     # -- measurement hooks ----------------------------------------------------
-    def timing(self, on=True):
-        _check(self._L.wsg_timing_enable(self._ctx, 1 if on else 0), "wsg_timing_enable")
+    def timing(self, on=True, every=1):
+        """Time the dominant kernel of every `every`-th batch call (HIP events)."""
+        _check(self._L.wsg_timing_enable(self._ctx, int(every) if on else 0), "wsg_timing_enable")
 
     def timing_read(self, reset=True):
         ms, n = ctypes.c_double(), ctypes.c_uint64()

@@ -14,13 +14,17 @@ struct wsg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     int num_cus = 256;
-    int blocks_per_cu = 8;
+    int blocks_per_cu = 32;   // measured best for the C2 unmask (tools/tune.py)
     unsigned long long* d_err = nullptr;
     // scratch
     uint32_t* d_tiles = nullptr;
     uint64_t tiles_cap = 0;
-    uint64_t* d_scan = nullptr;     // block_sums | block_prefix
-    uint64_t scan_cap = 0;          // entries per half
+    uint64_t* d_scan = nullptr;     // encode scan: sums | piece sums | prefixes | piece prefixes
+    uint64_t scan_cap = 0;          // blocks per quarter
+    uint32_t* d_piece_start = nullptr;   // encode: n + 1 piece starts
+    uint64_t piece_start_cap = 0;
+    uint32_t* d_piece_frame = nullptr;   // encode: piece -> frame
+    uint64_t piece_frame_cap = 0;
     // staging for host entry points
     uint8_t* d_stage = nullptr;
     uint8_t* h_stage = nullptr;
@@ -32,7 +36,8 @@ struct wsg_ctx {
     struct EvPair {
         hipEvent_t a, b;
     };
-    bool timing = false;
+    int timing = 0;            // 0 off; k > 0: time every k-th dominant-kernel launch
+    uint64_t timing_seq = 0;
     std::vector<EvPair> pending, pool;
     double acc_ms = 0.0;
     uint64_t launches = 0;
@@ -85,9 +90,27 @@ int ensure_scan(wsg_ctx* c, uint64_t blocks)
         WSG_HIP(hipFree(c->d_scan));
     c->d_scan = nullptr;
     c->scan_cap = 0;
-    if (hipMalloc(&c->d_scan, 2 * blocks * sizeof(uint64_t)) != hipSuccess)
+    if (hipMalloc(&c->d_scan, 4 * blocks * sizeof(uint64_t)) != hipSuccess)
         return WSG_ENOMEM;
     c->scan_cap = blocks;
+    return WSG_OK;
+}
+
+// grow a device array of T to at least `want` entries
+template <class T>
+int ensure_array(T*& ptr, uint64_t& cap, uint64_t want)
+{
+    want = std::max<uint64_t>(want, 1);
+    if (want <= cap)
+        return WSG_OK;
+    WSG_HIP(hipDeviceSynchronize());
+    if (ptr)
+        WSG_HIP(hipFree(ptr));
+    ptr = nullptr;
+    cap = 0;
+    if (hipMalloc(&ptr, want * sizeof(T)) != hipSuccess)
+        return WSG_ENOMEM;
+    cap = want;
     return WSG_OK;
 }
 
@@ -130,7 +153,7 @@ int ensure_stage(wsg_ctx* c, uint64_t bytes, uint64_t frames)
 // Record the start event of a timed kernel; returns the pair index or -1.
 int timing_begin(wsg_ctx* c, hipStream_t s)
 {
-    if (!c->timing)
+    if (c->timing <= 0 || (c->timing_seq++ % uint64_t(c->timing)) != 0)
         return -1;
     wsg_ctx::EvPair ev;
     if (!c->pool.empty()) {
@@ -213,7 +236,7 @@ int wsg_create(int device, wsg_ctx** out)
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (const char* e = std::getenv("WSG_BLOCKS_PER_CU")) {
         const int v = std::atoi(e);
-        if (v > 0 && v <= 32)
+        if (v > 0 && v <= 256)
             c->blocks_per_cu = v;
     }
     *out = c;
@@ -238,6 +261,8 @@ int wsg_destroy(wsg_ctx* c)
     (void)hipFree(c->d_err);
     (void)hipFree(c->d_tiles);
     (void)hipFree(c->d_scan);
+    (void)hipFree(c->d_piece_start);
+    (void)hipFree(c->d_piece_frame);
     (void)hipFree(c->d_stage);
     (void)hipFree(c->d_fs);
     (void)hipFree(c->d_info);
@@ -304,17 +329,20 @@ int wsg_encode_batch(wsg_ctx* c, const uint8_t* d_payload, const wsg_send_desc* 
         WSG_HIP(hipMemsetAsync(d_wire_off, 0, sizeof(uint64_t), s));
         return WSG_OK;
     }
-    const uint64_t tiles_cap = ceil_div(wire_cap, wsg::TILE);
+    // upper bound of the pieces: sum of ceil((size + 15) / PIECE) over frames
+    const uint64_t pieces_cap = wire_cap / wsg::PIECE + 2 * uint64_t(n) + 1;
     const uint64_t nb = ceil_div(n, wsg::SCAN_ITEMS);
-    if (int rc = ensure_tiles(c, tiles_cap))
-        return rc;
     if (int rc = ensure_scan(c, nb))
         return rc;
-    WSG_HIP(wsg::launch_encode_scan(s, d_desc, n, d_wire_off, c->d_scan, c->d_scan + c->scan_cap, c->d_tiles,
-                                    tiles_cap, wire_cap, c->d_err));
+    if (int rc = ensure_array(c->d_piece_start, c->piece_start_cap, uint64_t(n) + 1))
+        return rc;
+    if (int rc = ensure_array(c->d_piece_frame, c->piece_frame_cap, pieces_cap))
+        return rc;
+    WSG_HIP(wsg::launch_encode_scan(s, d_desc, n, d_wire_off, c->d_piece_start, c->d_scan, c->d_piece_frame,
+                                    pieces_cap, wire_cap, c->d_err));
     const int t = timing_begin(c, s);
-    WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, tiles_cap), d_payload, d_desc, n, d_wire_off, c->d_tiles, d_wire,
-                                    wire_cap));
+    WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, ceil_div(pieces_cap, wsg::BLOCK / 64)), d_payload, d_desc, n,
+                                    d_wire_off, c->d_piece_start, c->d_piece_frame, d_wire, wire_cap));
     timing_end(c, s, t);
     return WSG_OK;
 }
@@ -334,7 +362,8 @@ int wsg_fanout_encode(wsg_ctx* c, const uint8_t* d_payload, uint64_t len, const 
         return WSG_ENOMEM;
     hipStream_t s = pick(c, stream);
     const int t = timing_begin(c, s);
-    WSG_HIP(wsg::launch_fanout(s, grid_for(c, ceil_div(total, wsg::TILE)), d_payload, len, d_keys, k, opcode,
+    const uint64_t pieces = uint64_t(k) * ((fsize + 15 + wsg::PIECE - 1) / wsg::PIECE);
+    WSG_HIP(wsg::launch_fanout(s, grid_for(c, ceil_div(pieces, wsg::BLOCK / 64)), d_payload, len, d_keys, k, opcode,
                                mask ? 1u : 0u, fsize, d_wire));
     timing_end(c, s, t);
     return WSG_OK;
@@ -411,7 +440,8 @@ int wsg_timing_enable(wsg_ctx* c, int on)
 {
     if (!c)
         return WSG_EINVAL;
-    c->timing = on != 0;
+    c->timing = on > 0 ? on : 0;
+    c->timing_seq = 0;
     return WSG_OK;
 }
 

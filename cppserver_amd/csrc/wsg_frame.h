@@ -8,7 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../include/wsg_capi.h"
+#include "wsg_capi.h"
 
 #define WSG_HD __host__ __device__ __forceinline__
 

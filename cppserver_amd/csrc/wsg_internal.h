@@ -10,6 +10,8 @@ constexpr int BLOCK = 256;                  // 4 wave64s
 constexpr int CHUNK = 16;                   // bytes per lane per step (dwordx4)
 constexpr int UNROLL = 4;                   // steps per lane per tile
 constexpr uint64_t TILE = uint64_t(BLOCK) * CHUNK * UNROLL;   // 16 KiB of output
+constexpr int EU = 4;                                   // encode: 16-B steps per lane per piece
+constexpr uint64_t PIECE = uint64_t(64) * CHUNK * EU;   // encode work piece: 4 KiB of one frame
 constexpr int SCAN_PER_LANE = 4;
 constexpr uint64_t SCAN_ITEMS = uint64_t(BLOCK) * SCAN_PER_LANE;   // frames per scan block
 
@@ -19,18 +21,6 @@ __global__ void k_decode_parse(const uint8_t* wire, uint64_t wire_len, const uin
 __global__ void k_decode_unmask(const uint8_t* wire, uint8_t* out, uint64_t wire_len, const uint64_t* fs,
                                 const wsg_recv_info* info, uint32_t n, const uint32_t* tile_first,
                                 uint64_t num_tiles);
-__global__ void k_encode_scan_local(const wsg_send_desc* desc, uint32_t n, uint64_t* wire_off,
-                                    uint64_t* block_sums);
-__global__ void k_encode_scan_blocks(const uint64_t* block_sums, uint32_t nb, uint64_t* block_prefix,
-                                     uint64_t* wire_off, uint32_t n);
-__global__ void k_encode_finalize(const wsg_send_desc* desc, uint32_t n, uint64_t* wire_off,
-                                  const uint64_t* block_prefix, uint32_t* tile_first, uint64_t tiles_cap,
-                                  uint64_t wire_cap, unsigned long long* err);
-__global__ void k_encode_mask(const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
-                              const uint64_t* wire_off, const uint32_t* tile_first, uint8_t* wire,
-                              uint64_t wire_cap);
-__global__ void k_fanout(const uint8_t* payload, uint64_t len, const uint32_t* keys, uint32_t k, uint8_t opcode,
-                         uint32_t mask, uint64_t fsize, double inv_fsize, uint8_t* wire);
 __global__ void k_xor(const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key, uint32_t phase);
 
 // Host launchers (defined in wsg_kernels.hip next to the kernels).
@@ -40,12 +30,14 @@ hipError_t launch_decode_parse(hipStream_t s, const uint8_t* wire, uint64_t wire
 hipError_t launch_decode_unmask(hipStream_t s, int grid, const uint8_t* wire, uint8_t* out, uint64_t wire_len,
                                 const uint64_t* fs, const wsg_recv_info* info, uint32_t n,
                                 const uint32_t* tile_first, uint64_t num_tiles);
+// Sizes + piece counts scan (scan: 4 * ceil(n / SCAN_ITEMS) words), wire
+// offsets, piece starts (n + 1 each) and the piece -> frame map.
 hipError_t launch_encode_scan(hipStream_t s, const wsg_send_desc* desc, uint32_t n, uint64_t* wire_off,
-                              uint64_t* block_sums, uint64_t* block_prefix, uint32_t* tile_first,
-                              uint64_t tiles_cap, uint64_t wire_cap, unsigned long long* err);
+                              uint32_t* piece_start, uint64_t* scan, uint32_t* piece_frame, uint64_t pieces_cap,
+                              uint64_t wire_cap, unsigned long long* err);
 hipError_t launch_encode_mask(hipStream_t s, int grid, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
-                              const uint64_t* wire_off, const uint32_t* tile_first, uint8_t* wire,
-                              uint64_t wire_cap);
+                              const uint64_t* wire_off, const uint32_t* piece_start, const uint32_t* piece_frame,
+                              uint8_t* wire, uint64_t wire_cap);
 hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64_t len, const uint32_t* keys,
                          uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire);
 hipError_t launch_xor(hipStream_t s, int grid, const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,

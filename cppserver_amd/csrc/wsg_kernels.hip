@@ -116,6 +116,36 @@ __device__ __forceinline__ void store_partial(uint8_t* dst, v4u w, uint32_t nbyt
 
 __device__ __forceinline__ uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
+constexpr int LDSF = BLOCK;   // frames a tile may touch and still take the LDS-staged path
+
+__device__ __forceinline__ uint64_t lane_bcast(uint64_t v, int src)
+{
+    const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(v), src);
+    const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(v >> 32), src);
+    return uint64_t(lo) | (uint64_t(hi) << 32);
+}
+
+// tile_first[t] = frame for t in [lo, hi), for every lane's range, with the
+// whole wave storing each range (one lane per frame would serialise a large
+// frame's thousands of tiles on a single lane).
+__device__ __forceinline__ void fill_tiles_wave(uint32_t* tile_first, uint64_t lo, uint64_t hi, uint32_t frame)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    constexpr uint64_t kShort = 16;   // ranges up to this many entries: the lane stores its own
+    if (hi > lo && hi - lo <= kShort)
+        for (uint64_t t = lo; t < hi; ++t)
+            tile_first[t] = frame;
+    uint64_t pending = __ballot(hi > lo + kShort);
+    while (pending) {
+        const int j = __builtin_ctzll(pending);
+        pending &= pending - 1;
+        const uint64_t a = lane_bcast(lo, j), b = lane_bcast(hi, j);
+        const uint32_t fj = __builtin_amdgcn_readlane(frame, j);
+        for (uint64_t t = a + lane; t < b; t += 64)
+            tile_first[t] = fj;
+    }
+}
+
 __device__ __forceinline__ uint64_t lane_off(int u) { return (uint64_t(u) * BLOCK + threadIdx.x) * CHUNK; }
 
 // Last index in [lo, hi] whose start <= p; lo - 1 (possibly -1) if none.
@@ -180,44 +210,43 @@ __global__ __launch_bounds__(BLOCK) void k_decode_parse(const uint8_t* __restric
                                                         uint32_t* __restrict__ tile_first, uint64_t num_tiles,
                                                         unsigned long long* err)
 {
+    if (blockIdx.x * BLOCK + (threadIdx.x & ~63u) >= n)
+        return;   // whole wave past the last frame
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n)
-        return;
-    const uint64_t s = fs[i];
-    const uint64_t limit = (i + 1 < n) ? fs[i + 1] : wire_len;
-    wsg_recv_info r = {};
-    int e = WSG_ETRUNC;
-    if (s < wire_len) {
-        const uint64_t avail = wire_len - s;
-        const uint64_t a0 = s & ~uint64_t(15);
-        const v4u lo = ld16(wire + a0);
-        const v4u hi = (a0 + 16 < wire_len) ? ld16(wire + a0 + 16) : v4u{0, 0, 0, 0};
-        const v4u h = funnel(lo, hi, uint32_t(s & 15));   // wire[s .. s+16)
-        e = parse_header([&](uint32_t k) { return uint8_t(lane_byte(h, k)); }, avail, r);
-        if (e == 0) {
-            if (r.len > avail - r.hdr_len)
-                e = WSG_ETRUNC;
-            else if (limit < s || limit - s < r.hdr_len || r.len > limit - s - r.hdr_len)
-                e = WSG_EINVAL;   // the next frame starts inside this one
+    uint64_t lo_t = 0, hi_t = 0;
+    if (i < n) {
+        const uint64_t s = fs[i];
+        const uint64_t limit = (i + 1 < n) ? fs[i + 1] : wire_len;
+        wsg_recv_info r = {};
+        int e = WSG_ETRUNC;
+        if (s < wire_len) {
+            const uint64_t avail = wire_len - s;
+            const uint64_t a0 = s & ~uint64_t(15);
+            const v4u lo = ld16(wire + a0);
+            const v4u hi = (a0 + 16 < wire_len) ? ld16(wire + a0 + 16) : v4u{0, 0, 0, 0};
+            const v4u h = funnel(lo, hi, uint32_t(s & 15));   // wire[s .. s+16)
+            e = parse_header([&](uint32_t k) { return uint8_t(lane_byte(h, k)); }, avail, r);
+            if (e == 0) {
+                if (r.len > avail - r.hdr_len)
+                    e = WSG_ETRUNC;
+                else if (limit < s || limit - s < r.hdr_len || r.len > limit - s - r.hdr_len)
+                    e = WSG_EINVAL;   // the next frame starts inside this one
+            }
         }
+        if (e != 0) {
+            r = wsg_recv_info{};
+            r.payload_off = s;
+            r.error = int8_t(e);
+            atomicMin(err, (static_cast<unsigned long long>(i) << 8) | static_cast<unsigned long long>(-e));
+        } else {
+            r.payload_off = s + r.hdr_len;
+        }
+        info[i] = r;
+        // tiles whose first byte falls in [s, next start) belong to frame i
+        lo_t = (i == 0) ? 0 : ceil_div(s, TILE);
+        hi_t = min((i + 1 < n) ? ceil_div(limit, TILE) : num_tiles, num_tiles);
     }
-    if (e != 0) {
-        r = wsg_recv_info{};
-        r.payload_off = s;
-        r.error = int8_t(e);
-        atomicMin(err, (static_cast<unsigned long long>(i) << 8) | static_cast<unsigned long long>(-e));
-    } else {
-        r.payload_off = s + r.hdr_len;
-    }
-    info[i] = r;
-
-    // tiles whose first byte falls in [s, next start) belong to frame i
-    const uint64_t lo_t = (i == 0) ? 0 : ceil_div(s, TILE);
-    uint64_t hi_t = (i + 1 < n) ? ceil_div(limit, TILE) : num_tiles;
-    if (hi_t > num_tiles)
-        hi_t = num_tiles;
-    for (uint64_t t = lo_t; t < hi_t; ++t)
-        tile_first[t] = i;
+    fill_tiles_wave(tile_first, lo_t, hi_t, i);
 }
 
 namespace {
@@ -365,7 +394,54 @@ __global__ __launch_bounds__(BLOCK) void k_decode_unmask(const uint8_t* __restri
             continue;
         }
 
-        // dense: many tiny frames in this tile
+        if (f_hi - f < LDSF) {
+            // many frames: stage their records in LDS, binary-search per chunk
+            __shared__ uint64_t s_st[LDSF], s_po[LDSF], s_pe[LDSF];
+            __shared__ uint32_t s_key[LDSF];
+            const int cnt = int(f_hi - f) + 1;
+            __syncthreads();   // the previous tile's readers are done
+            if (int(threadIdx.x) < cnt) {
+                const uint32_t k = f + threadIdx.x;
+                s_st[threadIdx.x] = fs[k];
+                s_po[threadIdx.x] = info[k].payload_off;
+                s_pe[threadIdx.x] = info[k].payload_off + info[k].len;
+                s_key[threadIdx.x] = info[k].key;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const uint64_t p = base + lane_off(u);
+                int j = -1;
+                if (s_st[0] <= p) {
+                    int lo = 0, hi = cnt - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (s_st[mid] <= p)
+                            lo = mid;
+                        else
+                            hi = mid - 1;
+                    }
+                    j = lo;
+                }
+                if (j >= 0 && p >= s_po[j] && p + CHUNK <= s_pe[j]) {
+                    st16nt(out + p, v[u] ^ key_rot(s_key[j], uint32_t(p - s_po[j])));
+                } else {
+                    v4u w = v[u];
+#pragma unroll
+                    for (uint32_t b = 0; b < CHUNK; ++b) {
+                        const uint64_t q = p + b;
+                        while (j + 1 < cnt && s_st[j + 1] <= q)
+                            ++j;
+                        if (j >= 0 && q >= s_po[j] && q < s_pe[j])
+                            w[b >> 2] ^= uint32_t(key_byte(s_key[j], q - s_po[j])) << (8u * (b & 3u));
+                    }
+                    st16nt(out + p, w);
+                }
+            }
+            continue;
+        }
+
+        // dense: more frames than the LDS stage holds (tiny frames)
 #pragma unroll 1
         for (int u = 0; u < UNROLL; ++u)
             decode_chunk_generic(wire, out, wire_len, fs, info, n, f, f_hi, base + lane_off(u));
@@ -373,12 +449,22 @@ __global__ __launch_bounds__(BLOCK) void k_decode_unmask(const uint8_t* __restri
 }
 
 // ===========================================================================
-// Encode
+// Encode: frame-aligned work pieces
 // ===========================================================================
+//
+// A piece is at most PIECE = 4 KiB of ONE frame's wire bytes, cut at absolute
+// 16-byte chunk boundaries: piece k of frame i covers
+//     [max(off_i, A_i + k*PIECE), min(end_i, A_i + (k+1)*PIECE)),   A_i = off_i & ~15.
+// One wave encodes one piece, so the key, the key phase and the source shift
+// are uniform over it: full data chunks stream (aligned 16-B loads,
+// v_alignbyte_b32 funnel, XOR, 16-B nontemporal store).  Chunks holding
+// header / close-status bytes, and the two edge chunks a frame shares with
+// its neighbours, are built bytewise (edge chunks: each frame stores only
+// its own bytes).  Piece counts are scanned together with frame sizes.
 
 namespace {
 
-// Everything the mask kernel needs about one output frame.
+// Everything a piece needs about its frame (wave-uniform).
 struct FrameRec {
     uint64_t off;       // wire offset of the frame
     uint64_t pw;        // wire offset of the payload (status prefix included)
@@ -414,296 +500,209 @@ __device__ __forceinline__ FrameRec make_rec(uint64_t off, const uint8_t* src, u
     return r;
 }
 
-// Frames described by wsg_send_desc[] with scanned wire offsets.
-struct DescLayout {
-    static constexpr bool kNtSource = true;   // each payload byte is read once
-    const uint8_t* payload;
-    const wsg_send_desc* desc;
-    const uint64_t* wire_off;   // n + 1 entries
-    const uint32_t* tile_first;
-    uint32_t n;
-
-    __device__ FrameRec rec(int64_t o) const
-    {
-        const wsg_send_desc d = desc[o];
-        return make_rec(wire_off[o], payload + d.src_off, d.len, d.key, d.status, d.opcode, d.mask != 0);
-    }
-    __device__ int64_t first(uint64_t t) const { return min(tile_first[t], n - 1); }
-    __device__ int64_t owner(uint64_t p, int64_t f, int64_t f_hi) const { return owner_search(wire_off, f, f_hi, p); }
-    __device__ int64_t last_in_tile(uint64_t t, uint64_t num_tiles, int64_t f, uint64_t) const
-    {
-        int64_t h = (t + 1 < num_tiles) ? int64_t(min(tile_first[t + 1], n - 1)) : int64_t(n) - 1;
-        return h < f ? f : h;
-    }
-};
-
-// k frames of one payload, one key each (client-style fan-out).
-struct FanoutLayout {
-    static constexpr bool kNtSource = false;  // the payload is re-read by every frame: keep it in L2
-    const uint8_t* payload;
-    const uint32_t* keys;
-    uint64_t len;
-    uint64_t fsize;
-    double inv_fsize;
-    uint32_t n;
-    uint8_t opcode;
-    bool mask;
-
-    __device__ FrameRec rec(int64_t o) const
-    {
-        return make_rec(uint64_t(o) * fsize, payload, len, keys[o], 0, opcode, mask);
-    }
-    __device__ int64_t div(uint64_t p) const
-    {
-        int64_t o = int64_t(double(p) * inv_fsize);
-        if (o > 0 && uint64_t(o) * fsize > p)
-            --o;
-        if (uint64_t(o + 1) * fsize <= p)
-            ++o;
-        return o < int64_t(n) ? o : int64_t(n) - 1;
-    }
-    __device__ int64_t first(uint64_t t) const { return div(t * TILE); }
-    __device__ int64_t owner(uint64_t p, int64_t, int64_t) const { return div(p); }
-    __device__ int64_t last_in_tile(uint64_t, uint64_t, int64_t, uint64_t tend) const { return div(tend - 1); }
-};
-
-// One 16-byte output chunk of frame o (or of the frames after it).
-template <class L>
-__device__ __forceinline__ void encode_chunk(const L& lay, uint8_t* wire, uint64_t p, uint64_t total, int64_t o)
+// Wire byte q (off <= q < end) of frame R (ws.cpp:222-270).
+__device__ __forceinline__ uint32_t frame_byte(const FrameRec& R, uint64_t q)
 {
-    FrameRec R = lay.rec(o);
-    if (p >= R.data_w && p + CHUNK <= R.end) {
-        const v4u v = ld16_unaligned<L::kNtSource>(R.src + (p - R.data_w));
-        st16nt(wire + p, v ^ key_rot(R.key, uint32_t(p - R.pw)));
-        return;
-    }
-    const uint32_t nb = uint32_t(min<uint64_t>(CHUNK, total - p));
-    v4u w = {0, 0, 0, 0};
-    for (uint32_t j = 0; j < nb; ++j) {
-        const uint64_t q = p + j;
-        while (q >= R.end && o + 1 < int64_t(lay.n)) {
-            ++o;
-            R = lay.rec(o);
-        }
-        const uint64_t r = q - R.off;
-        uint32_t b;
-        if (r < R.hdr) {
-            b = header_byte(R.opcode, R.mask, R.body, R.key, uint32_t(r));
-        } else {
-            const uint64_t k = r - R.hdr;   // payload position (key index)
-            if (k < R.prefix)
-                b = uint32_t((k == 0 ? (R.status >> 8) : R.status) & 0xFF) ^ key_byte(R.key, k);
-            else
-                b = uint32_t(R.src[k - R.prefix]) ^ key_byte(R.key, k);
-        }
-        put_byte(w, j, b);
-    }
-    if (nb == CHUNK)
-        st16nt(wire + p, w);
-    else
-        store_partial(wire + p, w, nb);
+    const uint64_t r = q - R.off;
+    if (r < R.hdr)
+        return header_byte(R.opcode, R.mask, R.body, R.key, uint32_t(r));
+    const uint64_t k = r - R.hdr;   // payload position: key index from the payload start
+    if (k < R.prefix)
+        return uint32_t((k == 0 ? (R.status >> 8) : R.status) & 0xFF) ^ key_byte(R.key, k);
+    return uint32_t(R.src[k - R.prefix]) ^ key_byte(R.key, k);
 }
 
-// What the boundary path keeps per frame (data-chunk test and source).
-struct EncFrames {
-    v4u64 st;    // frame start (~0 when absent)
-    v4u64 dw;    // first data byte
-    v4u64 end;   // one past the frame
-    v4u64 pw;    // payload start (key phase origin)
-    v4u64 sb;    // address of (src - data_w): source of wire byte q is sb + q
-    v4u key;
-};
+__device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-template <class L>
-__device__ __forceinline__ void encode_tiles(const L& lay, uint8_t* wire, uint64_t total)
+// One wave writes piece k of frame R.
+template <bool NT>
+__device__ __forceinline__ void encode_piece(const FrameRec& R, uint64_t k, uint8_t* __restrict__ wire)
 {
-    const uint64_t num_tiles = (total + TILE - 1) / TILE;
-    for (uint64_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
-        const uint64_t base = t * TILE;
-        const uint64_t tend = min(base + TILE, total);
-        const bool full = (tend - base == TILE);
-        const int64_t f = lay.first(t);
-        const FrameRec R = lay.rec(f);
-        if (full && base >= R.data_w && tend <= R.end) {
-            // stream: the whole tile is data of frame f (uniform shift and key)
-            const uint8_t* src = R.src + (base - R.data_w);
-            const uint32_t k = key_rot(R.key, uint32_t(base - R.pw));
-            const uint32_t s = uint32_t(reinterpret_cast<uintptr_t>(src) & 15u);
-            const uint8_t* a0 = src - s;
-            v4u lo[UNROLL];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t lo = (R.off & ~uint64_t(15)) + k * PIECE;
+    if (lo >= R.end)
+        return;   // piece counts are an upper bound
+    const uint64_t hi = min(lo + PIECE, R.end);
+    const uintptr_t sbase = reinterpret_cast<uintptr_t>(R.src) - R.data_w;   // source of wire byte q: sbase + q
+    const uint32_t s = uint32_t((sbase + lo) & 15u);                        // uniform: lo, p are 16-aligned
+    const uint32_t kw = key_rot(R.key, uint32_t(lo - R.pw));                 // uniform phase (mod 4)
+    bool data[EU];
+    v4u a[EU], b[EU];
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
-                lo[u] = L::kNtSource ? ld16nt(a0 + lane_off(u)) : ld16(a0 + lane_off(u));
-            if (s != 0) {
-                v4u hi[UNROLL];
+    for (int u = 0; u < EU; ++u) {
+        const uint64_t p = lo + (uint64_t(u) * 64 + lane) * CHUNK;
+        data[u] = p < hi && p >= R.data_w && p + CHUNK <= R.end;
+        const uint8_t* a0 = reinterpret_cast<const uint8_t*>(sbase + p - s);
+        a[u] = data[u] ? (NT ? ld16nt(a0) : ld16(a0)) : v4u{0, 0, 0, 0};
+    }
+    if (s != 0) {
 #pragma unroll
-                for (int u = 0; u < UNROLL; ++u)
-                    hi[u] = L::kNtSource ? ld16nt(a0 + lane_off(u) + CHUNK) : ld16(a0 + lane_off(u) + CHUNK);
-#pragma unroll
-                for (int u = 0; u < UNROLL; ++u)
-                    lo[u] = funnel(lo[u], hi[u], s);
-            }
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
-                st16nt(wire + base + lane_off(u), lo[u] ^ k);
-            continue;
+        for (int u = 0; u < EU; ++u) {
+            const uint64_t p = lo + (uint64_t(u) * 64 + lane) * CHUNK;
+            const uint8_t* a0 = reinterpret_cast<const uint8_t*>(sbase + p - s);
+            b[u] = data[u] ? (NT ? ld16nt(a0 + CHUNK) : ld16(a0 + CHUNK)) : v4u{0, 0, 0, 0};
         }
-        const int64_t f_hi = lay.last_in_tile(t, num_tiles, f, tend);
-        if (full && f_hi - f < MAXF) {
-            // boundary: frames f..f_hi from registers
-            EncFrames F;
+    }
 #pragma unroll
-            for (int k = 0; k < MAXF; ++k) {
-                if (f + k <= f_hi) {
-                    const FrameRec Rk = (k == 0) ? R : lay.rec(f + k);
-                    F.st[k] = Rk.off;
-                    F.dw[k] = Rk.data_w;
-                    F.end[k] = Rk.end;
-                    F.pw[k] = Rk.pw;
-                    F.sb[k] = reinterpret_cast<uintptr_t>(Rk.src) - Rk.data_w;
-                    F.key[k] = Rk.key;
-                } else {
-                    F.st[k] = ~uint64_t(0);
-                    F.dw[k] = F.end[k] = F.pw[k] = 0;
-                    F.sb[k] = 0;
-                    F.key[k] = 0;
-                }
+    for (int u = 0; u < EU; ++u) {
+        const uint64_t p = lo + (uint64_t(u) * 64 + lane) * CHUNK;
+        if (data[u]) {
+            st16nt(wire + p, (s ? funnel(a[u], b[u], s) : a[u]) ^ kw);
+        } else if (p < hi) {
+            // header / status bytes, or an edge chunk shared with a neighbour
+            const uint64_t qlo = max(p, R.off), qhi = min(p + CHUNK, R.end);
+            if (qlo == p && qhi == p + CHUNK) {
+                v4u w = {0, 0, 0, 0};
+                for (uint32_t j = 0; j < CHUNK; ++j)
+                    put_byte(w, j, frame_byte(R, p + j));
+                st16nt(wire + p, w);
+            } else {
+                for (uint64_t q = qlo; q < qhi; ++q)
+                    wire[q] = uint8_t(frame_byte(R, q));
             }
-            // all source loads of the lane first, then the stores
-            v4u v[UNROLL];
-            int js[UNROLL];
-            bool data[UNROLL];
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const uint64_t p = base + lane_off(u);
-                int j = 0;
-#pragma unroll
-                for (int k = 1; k < MAXF; ++k)
-                    j = (F.st[k] <= p) ? k : j;
-                js[u] = j;
-                data[u] = p >= pick(F.dw, j) && p + CHUNK <= pick(F.end, j);
-                v[u] = data[u] ? ld16_unaligned<L::kNtSource>(reinterpret_cast<const uint8_t*>(pick(F.sb, j) + p)) : v4u{0, 0, 0, 0};
-            }
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const uint64_t p = base + lane_off(u);
-                const int j = js[u];
-                if (data[u])
-                    st16nt(wire + p, v[u] ^ key_rot(pick(F.key, j), uint32_t(p - pick(F.pw, j))));
-                else
-                    encode_chunk(lay, wire, p, total, f + j);   // header bytes: rare
-            }
-            continue;
-        }
-        // dense tiles and the last partial tile
-#pragma unroll 1
-        for (int u = 0; u < UNROLL; ++u) {
-            const uint64_t p = base + lane_off(u);
-            if (p >= tend)
-                break;
-            encode_chunk(lay, wire, p, total, lay.owner(p, f, f_hi));
         }
     }
 }
+
+__device__ __forceinline__ uint64_t pieces_of(uint64_t frame_bytes) { return (frame_bytes + 15 + PIECE - 1) / PIECE; }
 
 } // namespace
 
-// Per-block local exclusive scan of frame sizes (SCAN_ITEMS frames / block).
+// Per-block local exclusive scans of frame sizes and piece counts
+// (SCAN_ITEMS frames per block).
 __global__ __launch_bounds__(BLOCK) void k_encode_scan_local(const wsg_send_desc* __restrict__ desc, uint32_t n,
                                                              uint64_t* __restrict__ wire_off,
-                                                             uint64_t* __restrict__ block_sums)
+                                                             uint32_t* __restrict__ piece_start,
+                                                             uint64_t* __restrict__ block_sums,
+                                                             uint64_t* __restrict__ block_psums)
 {
     const uint64_t first = uint64_t(blockIdx.x) * SCAN_ITEMS + uint64_t(threadIdx.x) * SCAN_PER_LANE;
-    uint64_t sz[SCAN_PER_LANE];
-    uint64_t mine = 0;
+    uint64_t sz[SCAN_PER_LANE], pc[SCAN_PER_LANE];
+    uint64_t mine = 0, mine_p = 0;
 #pragma unroll
     for (int k = 0; k < SCAN_PER_LANE; ++k) {
         const uint64_t i = first + k;
-        sz[k] = 0;
+        sz[k] = pc[k] = 0;
         if (i < n) {
             const wsg_send_desc d = desc[i];
             const SendGeom g = send_geom(d.opcode, d.mask != 0, d.len, d.status);
             sz[k] = g.hdr + g.body;
+            pc[k] = pieces_of(sz[k]);
         }
         mine += sz[k];
+        mine_p += pc[k];
     }
-    uint64_t total;
+    uint64_t total, total_p;
     uint64_t run = block_exclusive_scan(mine, &total);
+    uint64_t run_p = block_exclusive_scan(mine_p, &total_p);
 #pragma unroll
     for (int k = 0; k < SCAN_PER_LANE; ++k) {
         const uint64_t i = first + k;
-        if (i < n)
+        if (i < n) {
             wire_off[i] = run;
+            piece_start[i] = uint32_t(run_p);
+        }
         run += sz[k];
+        run_p += pc[k];
     }
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
         block_sums[blockIdx.x] = total;
+        block_psums[blockIdx.x] = total_p;
+    }
 }
 
-// Single block: exclusive scan of the block sums; wire_off[n] = total.
-__global__ __launch_bounds__(BLOCK) void k_encode_scan_blocks(const uint64_t* __restrict__ block_sums, uint32_t nb,
+// Single block: exclusive scans of the block sums; wire_off[n] = total bytes,
+// piece_start[n] = total pieces.
+__global__ __launch_bounds__(BLOCK) void k_encode_scan_blocks(const uint64_t* __restrict__ block_sums,
+                                                              const uint64_t* __restrict__ block_psums, uint32_t nb,
                                                               uint64_t* __restrict__ block_prefix,
-                                                              uint64_t* __restrict__ wire_off, uint32_t n)
+                                                              uint64_t* __restrict__ block_pprefix,
+                                                              uint64_t* __restrict__ wire_off,
+                                                              uint32_t* __restrict__ piece_start, uint32_t n)
 {
-    uint64_t carry = 0;
+    uint64_t carry = 0, carry_p = 0;
     for (uint32_t c = 0; c < nb; c += BLOCK) {
         const uint32_t i = c + threadIdx.x;
-        const uint64_t v = i < nb ? block_sums[i] : 0;
-        uint64_t tot;
-        const uint64_t ex = block_exclusive_scan(v, &tot);
-        if (i < nb)
+        uint64_t tot, tot_p;
+        const uint64_t ex = block_exclusive_scan(i < nb ? block_sums[i] : 0, &tot);
+        const uint64_t ex_p = block_exclusive_scan(i < nb ? block_psums[i] : 0, &tot_p);
+        if (i < nb) {
             block_prefix[i] = carry + ex;
+            block_pprefix[i] = carry_p + ex_p;
+        }
         carry += tot;
+        carry_p += tot_p;
     }
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
         wire_off[n] = carry;
+        piece_start[n] = uint32_t(carry_p);
+    }
 }
 
-// Add block prefixes, build the tile -> first-frame map, check capacity.
+// Add block prefixes, build the piece -> frame map, check capacity.
 __global__ __launch_bounds__(BLOCK) void k_encode_finalize(const wsg_send_desc* __restrict__ desc, uint32_t n,
                                                            uint64_t* __restrict__ wire_off,
+                                                           uint32_t* __restrict__ piece_start,
                                                            const uint64_t* __restrict__ block_prefix,
-                                                           uint32_t* __restrict__ tile_first, uint64_t tiles_cap,
+                                                           const uint64_t* __restrict__ block_pprefix,
+                                                           uint32_t* __restrict__ piece_frame, uint64_t pieces_cap,
                                                            uint64_t wire_cap, unsigned long long* err)
 {
+    if (blockIdx.x * BLOCK + (threadIdx.x & ~63u) >= n)
+        return;   // whole wave past the last frame
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n)
-        return;
-    const wsg_send_desc d = desc[i];
-    const SendGeom g = send_geom(d.opcode, d.mask != 0, d.len, d.status);
-    const uint64_t off = wire_off[i] + block_prefix[i / SCAN_ITEMS];
-    const uint64_t end = off + g.hdr + g.body;
-    wire_off[i] = off;
-    if (end > wire_cap)
-        atomicMin(err, (static_cast<unsigned long long>(i) << 8) | static_cast<unsigned long long>(-WSG_ENOMEM));
-    const uint64_t lo = (i == 0) ? 0 : ceil_div(off, TILE);
-    uint64_t hi = ceil_div(end, TILE);
-    if (hi > tiles_cap)
-        hi = tiles_cap;
-    for (uint64_t t = lo; t < hi; ++t)
-        tile_first[t] = i;
+    uint64_t lo = 0, hi = 0;
+    if (i < n) {
+        const wsg_send_desc d = desc[i];
+        const SendGeom g = send_geom(d.opcode, d.mask != 0, d.len, d.status);
+        const uint64_t off = wire_off[i] + block_prefix[i / SCAN_ITEMS];
+        const uint64_t ps = piece_start[i] + block_pprefix[i / SCAN_ITEMS];
+        const uint64_t end = off + g.hdr + g.body;
+        wire_off[i] = off;
+        piece_start[i] = uint32_t(ps);
+        if (end > wire_cap)
+            atomicMin(err, (static_cast<unsigned long long>(i) << 8) |
+                               static_cast<unsigned long long>(-WSG_ENOMEM));
+        lo = min(ps, pieces_cap);
+        hi = min(ps + pieces_of(g.hdr + g.body), pieces_cap);
+    }
+    fill_tiles_wave(piece_frame, lo, hi, i);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_encode_mask(const uint8_t* __restrict__ payload,
                                                        const wsg_send_desc* __restrict__ desc, uint32_t n,
                                                        const uint64_t* __restrict__ wire_off,
-                                                       const uint32_t* __restrict__ tile_first,
+                                                       const uint32_t* __restrict__ piece_start,
+                                                       const uint32_t* __restrict__ piece_frame,
                                                        uint8_t* __restrict__ wire, uint64_t wire_cap)
 {
-    const uint64_t total = wire_off[n];
-    if (total > wire_cap)
+    if (wire_off[n] > wire_cap)
         return;   // capacity error latched by k_encode_finalize
-    DescLayout lay{payload, desc, wire_off, tile_first, n};
-    encode_tiles(lay, wire, total);
+    const uint32_t pieces = piece_start[n];
+    const uint32_t waves = gridDim.x * (BLOCK / 64);
+    for (uint32_t q = blockIdx.x * (BLOCK / 64) + wave_id(); q < pieces; q += waves) {
+        const uint32_t i = piece_frame[q];
+        const wsg_send_desc d = desc[i];
+        const FrameRec R = make_rec(wire_off[i], payload + d.src_off, d.len, d.key, d.status, d.opcode, d.mask != 0);
+        encode_piece<true>(R, q - piece_start[i], wire);
+    }
 }
 
+// k client-style frames of one payload (one key each), back to back: pieces
+// map to frames arithmetically.  The payload is re-read by every frame, so
+// its loads keep the default cache policy (it stays in L2).
 __global__ __launch_bounds__(BLOCK) void k_fanout(const uint8_t* __restrict__ payload, uint64_t len,
                                                   const uint32_t* __restrict__ keys, uint32_t k, uint8_t opcode,
-                                                  uint32_t mask, uint64_t fsize, double inv_fsize,
-                                                  uint8_t* __restrict__ wire)
+                                                  uint32_t mask, uint64_t fsize, uint8_t* __restrict__ wire)
 {
-    FanoutLayout lay{payload, keys, len, fsize, inv_fsize, k, opcode, mask != 0};
-    encode_tiles(lay, wire, fsize * k);
+    const uint32_t per_frame = uint32_t(pieces_of(fsize));
+    const uint64_t pieces = uint64_t(per_frame) * k;
+    const uint64_t waves = uint64_t(gridDim.x) * (BLOCK / 64);
+    for (uint64_t q = uint64_t(blockIdx.x) * (BLOCK / 64) + wave_id(); q < pieces; q += waves) {
+        const uint32_t i = uint32_t(q / per_frame);
+        const FrameRec R = make_rec(uint64_t(i) * fsize, payload, len, keys[i], 0, opcode, mask != 0);
+        encode_piece<false>(R, q - uint64_t(i) * per_frame, wire);
+    }
 }
 
 // Single-buffer XOR used by the per-frame host path: dst[i] = src[i] ^
@@ -743,29 +742,33 @@ hipError_t launch_decode_unmask(hipStream_t s, int grid, const uint8_t* wire, ui
 }
 
 hipError_t launch_encode_scan(hipStream_t s, const wsg_send_desc* desc, uint32_t n, uint64_t* wire_off,
-                              uint64_t* block_sums, uint64_t* block_prefix, uint32_t* tile_first,
-                              uint64_t tiles_cap, uint64_t wire_cap, unsigned long long* err)
+                              uint32_t* piece_start, uint64_t* scan, uint32_t* piece_frame, uint64_t pieces_cap,
+                              uint64_t wire_cap, unsigned long long* err)
 {
     const uint32_t nb = uint32_t((n + SCAN_ITEMS - 1) / SCAN_ITEMS);
-    k_encode_scan_local<<<nb, BLOCK, 0, s>>>(desc, n, wire_off, block_sums);
-    k_encode_scan_blocks<<<1, BLOCK, 0, s>>>(block_sums, nb, block_prefix, wire_off, n);
-    k_encode_finalize<<<(n + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(desc, n, wire_off, block_prefix, tile_first,
-                                                                tiles_cap, wire_cap, err);
+    uint64_t* sums = scan;
+    uint64_t* psums = scan + nb;
+    uint64_t* prefix = scan + 2 * uint64_t(nb);
+    uint64_t* pprefix = scan + 3 * uint64_t(nb);
+    k_encode_scan_local<<<nb, BLOCK, 0, s>>>(desc, n, wire_off, piece_start, sums, psums);
+    k_encode_scan_blocks<<<1, BLOCK, 0, s>>>(sums, psums, nb, prefix, pprefix, wire_off, piece_start, n);
+    k_encode_finalize<<<(n + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(desc, n, wire_off, piece_start, prefix, pprefix,
+                                                                piece_frame, pieces_cap, wire_cap, err);
     return hipGetLastError();
 }
 
 hipError_t launch_encode_mask(hipStream_t s, int grid, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
-                              const uint64_t* wire_off, const uint32_t* tile_first, uint8_t* wire,
-                              uint64_t wire_cap)
+                              const uint64_t* wire_off, const uint32_t* piece_start, const uint32_t* piece_frame,
+                              uint8_t* wire, uint64_t wire_cap)
 {
-    k_encode_mask<<<grid, BLOCK, 0, s>>>(payload, desc, n, wire_off, tile_first, wire, wire_cap);
+    k_encode_mask<<<grid, BLOCK, 0, s>>>(payload, desc, n, wire_off, piece_start, piece_frame, wire, wire_cap);
     return hipGetLastError();
 }
 
 hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64_t len, const uint32_t* keys,
                          uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire)
 {
-    k_fanout<<<grid, BLOCK, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, 1.0 / double(fsize), wire);
+    k_fanout<<<grid, BLOCK, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, wire);
     return hipGetLastError();
 }
 

@@ -172,8 +172,9 @@ size_t wsg_session_required(wsg_session* s);
 int wsg_session_clear(wsg_session* s);
 
 /* ---- kernel timing (measurement hook used by bench.py) ------------------ */
-/* When enabled, the ctx records HIP events around the dominant payload kernel
- * of every batch call on the stream it is launched on.                        */
+/* on = k > 0: the ctx records HIP events around the dominant payload kernel of
+ * every k-th batch call, on the stream it is launched on (k > 1 keeps the
+ * event packets' own cost out of most steps); on = 0 disables.               */
 int wsg_timing_enable(wsg_ctx* ctx, int on);
 /* Sum of the dominant-kernel durations (ms) and launch count since the last
  * reset; synchronizes outstanding events.                                     */

@@ -1,0 +1,69 @@
+"""Interleaved A/B timing of decode variants on the GPU box (medians).
+
+usage: python tools/tune.py [bpc ...]    (env WSG_BLOCKS_PER_CU per context)
+Each context is created with its own WSG_BLOCKS_PER_CU; runs are interleaved
+so clock/thermal drift hits every setting alike (guide §5.4 rule 24).
+"""
+import os
+import statistics
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import cppserver_amd as ca  # noqa: E402
+from cppserver_amd import workloads as wl  # noqa: E402
+
+
+def main():
+    # settings: "BPC" or "BPC@path/to/libwsg.so"
+    settings = sys.argv[1:] or ["8", "16", "32"]
+    n, size = int(os.environ.get("FRAMES", 4096)), int(os.environ.get("SIZE", 65536))
+    wire, fs, _ = wl.c2_wire(n, size, seed=1)
+    w = torch.from_numpy(wire).cuda()
+    f = torch.from_numpy(fs.view(np.int64)).cuda()
+    out = torch.empty_like(w)
+    info = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    codecs = {}
+    for b in settings:
+        bpc, _, path = b.partition("@")
+        os.environ["WSG_BLOCKS_PER_CU"] = bpc
+        codecs[b] = ca.Codec(0, lib_path=path or None)
+    every = int(os.environ.get("EVERY", 1))
+    kern = {b: [] for b in settings}
+    step = {b: [] for b in settings}
+    bare = {b: [] for b in settings}
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for rep in range(int(os.environ.get("REPS", 7))):
+        for b in settings:
+            c = codecs[b]
+            for _ in range(3):
+                c.decode_batch(w, f, out=out, info=info)
+            e0.record()
+            for _ in range(20):
+                c.decode_batch(w, f, out=out, info=info)
+            e1.record()
+            e1.synchronize()
+            bare[b].append(e0.elapsed_time(e1) / 20)
+            c.timing(True, every)
+            c.timing_read()
+            e0.record()
+            for _ in range(20):
+                c.decode_batch(w, f, out=out, info=info)
+            e1.record()
+            e1.synchronize()
+            ms, k = c.timing_read()
+            c.timing(False)
+            kern[b].append(ms / k)
+            step[b].append(e0.elapsed_time(e1) / 20)
+    alg = 2 * len(wire)
+    for b in settings:
+        km, sm, bm = statistics.median(kern[b]), statistics.median(step[b]), statistics.median(bare[b])
+        print("%-40s kernel %.4f ms (%.0f GB/s)  step %.4f ms (%.0f GiB/s)  untimed step %.4f ms (%.0f GiB/s)  spread %.1f%%" % (
+            b, km, alg / km / 1e6, sm, n * size / (sm * 1e-3) / 2**30, bm, n * size / (bm * 1e-3) / 2**30,
+            100 * (max(kern[b]) - min(kern[b])) / km))
+
+
+if __name__ == "__main__":
+    main()
