@@ -110,6 +110,12 @@ class Workload:
             self.wire = torch.from_numpy(wire).to(device)
             self.fs = torch.from_numpy(fs.view(np.int64)).to(device)
             self.out = torch.empty_like(self.wire)
+            # steps alternate between two distinct batches (2 x 537 MB touched),
+            # so no step reads its input from the 256 MiB Infinity Cache that
+            # the previous step left warm: every step is fresh HBM traffic
+            wire2 = wl.c2_wire(n, size, seed=2000 + rank)[0]
+            self.batches = [(self.wire, self.out), (torch.from_numpy(wire2).to(device), torch.empty_like(self.wire))]
+            self.turn = 0
             self.info = torch.empty(n * ca.RECV_INFO.itemsize, dtype=torch.uint8, device=device)
             self.payload_bytes = n * size
             self.alg_bytes = 2 * len(wire)           # unmask kernel: read wire + write out
@@ -166,7 +172,9 @@ class Workload:
     def step(self):
         c = self.codec
         if self.cfg == "c2":
-            c.decode_batch(self.wire, self.fs, out=self.out, info=self.info)
+            wire, out = self.batches[self.turn]
+            self.turn ^= 1
+            c.decode_batch(wire, self.fs, out=out, info=self.info)
         elif self.cfg == "c3":
             c.encode_batch(self.payload, self.desc, wire=self.wire, wire_cap=self.cap, wire_off=self.woff)
             c.decode_batch(self.wire, self.woff[:-1], out=self.out, info=self.info)
@@ -180,6 +188,8 @@ class Workload:
         if self.cfg != "c2":
             return True
         wire, fs, keys = self.host
+        self.codec.decode_batch(self.wire, self.fs, out=self.out, info=self.info)
+        self.codec.sync()
         out = self.out.cpu().numpy()
         n = len(fs)
         fsz = len(wire) // n
@@ -252,6 +262,29 @@ def pcie_inclusive(w, reps=3):
     return w.payload_bytes / dt / GIB
 
 
+def gather_leg(w, world, device):
+    """C5's exchange step: every rank's framed output to rank 0 over RCCL
+    (variable-size grouped send/recv, cppserver_amd.shard.gather_frames),
+    timed once after the encode steps; reported beside the kernel rate."""
+    import torch
+
+    from cppserver_amd import shard
+
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    parts = shard.gather_frames(w.wire, w.woff)
+    torch.cuda.synchronize()
+    barrier(world)
+    dt = time.perf_counter() - t0
+    moved = None
+    if parts is not None:
+        moved = sum(int(p[1][-1].item()) for r, p in enumerate(parts) if r != 0)
+    dt = max_over_ranks(dt, world, device)
+    return {"ms": round(dt * 1e3, 3), "bytes_into_root": moved,
+            "GBps_into_root": round(moved / dt / 1e9, 1) if moved else None}
+
+
 def main():
     args = parse()
     import torch
@@ -293,6 +326,8 @@ def main():
     traffic = pmc_traffic(args.pmc, w.cfg)
 
     extras = {}
+    if w.cfg == "c5" and world > 1:
+        extras["gather"] = gather_leg(w, world, device)
     if rank == 0 and world == 1 and not args.no_extras:
         extras["copy_ceiling_GBps"] = round(copy_ceiling(w), 1)
         pc = pcie_inclusive(w)
@@ -319,7 +354,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if w.cfg == "c5" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded random payloads and keys)",

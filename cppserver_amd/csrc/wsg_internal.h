@@ -8,7 +8,10 @@ namespace wsg {
 
 constexpr int BLOCK = 256;                  // 4 wave64s
 constexpr int CHUNK = 16;                   // bytes per lane per step (dwordx4)
-constexpr int UNROLL = 4;                   // steps per lane per tile
+#ifndef WSG_UNROLL
+#define WSG_UNROLL 4
+#endif
+constexpr int UNROLL = WSG_UNROLL;          // steps per lane per tile
 constexpr uint64_t TILE = uint64_t(BLOCK) * CHUNK * UNROLL;   // 16 KiB of output
 constexpr int EU = 4;                                   // encode: 16-B steps per lane per piece
 constexpr uint64_t PIECE = uint64_t(64) * CHUNK * EU;   // encode work piece: 4 KiB of one frame

@@ -31,12 +31,41 @@ typedef uint64_t v4u64 __attribute__((ext_vector_type(4)));   // MAXF-wide frame
 
 constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary path
 
+// Streaming loads/stores carry the nontemporal hint (measured faster for
+// once-touched data on MI355X: tools/membench.hip); WSG_NT_LOAD/STORE=0
+// builds the plain-policy variants for A/B runs.
+#ifndef WSG_NT_LOAD
+#define WSG_NT_LOAD 1
+#endif
+#ifndef WSG_ENC_NT_SRC
+#define WSG_ENC_NT_SRC 0   // encode payload loads: plain policy measured 1-5% faster than nontemporal
+#endif
+#ifndef WSG_ENC_NT_HI
+#define WSG_ENC_NT_HI 1    // ... including the funnel's second block (the next lane's line)
+#endif
+#ifndef WSG_DIAG_ENC
+#define WSG_DIAG_ENC 0   // timing-only encode diagnostics: 1 skip edge chunks, 2 no funnel
+#endif
+#ifndef WSG_DIAG
+#define WSG_DIAG 0   // 1/2: timing-only diagnostic builds of k_decode_unmask (tools/)
+#endif
+#ifndef WSG_NT_STORE
+#define WSG_NT_STORE 1
+#endif
 __device__ __forceinline__ v4u ld16(const uint8_t* p) { return *reinterpret_cast<const v4u*>(p); }
 __device__ __forceinline__ v4u ld16nt(const uint8_t* p)
 {
-    return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    if (WSG_NT_LOAD)
+        return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    return ld16(p);
 }
-__device__ __forceinline__ void st16nt(uint8_t* p, v4u v) { __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p)); }
+__device__ __forceinline__ void st16nt(uint8_t* p, v4u v)
+{
+    if (WSG_NT_STORE)
+        __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
+    else
+        *reinterpret_cast<v4u*>(p) = v;
+}
 
 __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t b)
 {
@@ -270,6 +299,13 @@ __device__ __forceinline__ void decode_chunk_generic(const uint8_t* __restrict__
         }
     }
     const uint32_t nb = uint32_t(min<uint64_t>(CHUNK, wire_len - p));
+    v4u src = {0, 0, 0, 0};
+    if (nb == CHUNK) {
+        src = ld16(wire + p);
+    } else {
+        for (uint32_t j = 0; j < nb; ++j)
+            put_byte(src, j, wire[p + j]);   // the wire's last partial chunk only
+    }
     v4u w = {0, 0, 0, 0};
     for (uint32_t j = 0; j < nb; ++j) {
         const uint64_t q = p + j;
@@ -279,7 +315,7 @@ __device__ __forceinline__ void decode_chunk_generic(const uint8_t* __restrict__
             oplen = info[o].len;
             okey = info[o].key;
         }
-        uint32_t b = wire[q];
+        uint32_t b = lane_byte(src, j);
         if (o >= 0 && q >= opoff && q - opoff < oplen)
             b ^= key_byte(okey, q - opoff);
         put_byte(w, j, b);
@@ -342,10 +378,22 @@ __global__ __launch_bounds__(BLOCK) void k_decode_unmask(const uint8_t* __restri
         for (int u = 0; u < UNROLL; ++u)
             v[u] = ld16nt(wire + base + lane_off(u));
 
+#if WSG_DIAG == 2   // diagnostic build (timing only, wrong output): no metadata at all
+        {
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u)
+                st16nt(out + base + lane_off(u), v[u] ^ uint32_t(t));
+            continue;
+        }
+#endif
         const uint64_t poff = info[f].payload_off;
         const uint64_t pend = poff + info[f].len;
         const uint32_t key = info[f].key;
+#if WSG_DIAG == 1   // diagnostic build (timing only, wrong output): every tile streams
+        if (true) {
+#else
         if (base >= poff && tend <= pend) {
+#endif
             // stream: the whole tile is payload of frame f
             const uint32_t k = key_rot(key, uint32_t(base - poff));
 #pragma unroll
@@ -500,69 +548,144 @@ __device__ __forceinline__ FrameRec make_rec(uint64_t off, const uint8_t* src, u
     return r;
 }
 
-// Wire byte q (off <= q < end) of frame R (ws.cpp:222-270).
-__device__ __forceinline__ uint32_t frame_byte(const FrameRec& R, uint64_t q)
+// A descriptor read as eight dwords: scalar loads cannot fetch the u8 fields
+// on gfx9, and a vector load for them would bring an s_waitcnt vmcnt(0)
+// that also waits for every data load in flight.
+struct Desc {
+    uint64_t src_off, len;
+    uint32_t key;
+    int32_t status;
+    uint8_t opcode;
+    bool mask;
+};
+
+__device__ __forceinline__ Desc load_desc(const wsg_send_desc* d)
 {
-    const uint64_t r = q - R.off;
-    if (r < R.hdr)
-        return header_byte(R.opcode, R.mask, R.body, R.key, uint32_t(r));
-    const uint64_t k = r - R.hdr;   // payload position: key index from the payload start
-    if (k < R.prefix)
-        return uint32_t((k == 0 ? (R.status >> 8) : R.status) & 0xFF) ^ key_byte(R.key, k);
-    return uint32_t(R.src[k - R.prefix]) ^ key_byte(R.key, k);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(d);
+    Desc r;
+    r.src_off = uint64_t(w[0]) | (uint64_t(w[1]) << 32);
+    r.len = uint64_t(w[2]) | (uint64_t(w[3]) << 32);
+    r.key = w[4];
+    r.status = int32_t(w[5]);
+    r.opcode = uint8_t(w[6]);
+    r.mask = ((w[6] >> 8) & 0xFFu) != 0;
+    return r;
 }
+static_assert(offsetof(wsg_send_desc, key) == 16 && offsetof(wsg_send_desc, opcode) == 24 &&
+                  offsetof(wsg_send_desc, mask) == 25,
+              "wsg_send_desc layout");
 
 __device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-// One wave writes piece k of frame R.
-template <bool NT>
-__device__ __forceinline__ void encode_piece(const FrameRec& R, uint64_t k, uint8_t* __restrict__ wire)
+// A chunk of frame R that is not all data (it holds header / close-status
+// bytes, or it is shared with a neighbouring frame).  Its data bytes come
+// from one 32-byte source window read with at most two aligned 16-B loads
+// (only blocks that hold a byte of this frame's data are touched); all 16
+// bytes are built in registers, then stored with one 16-B store, or, for a
+// chunk shared with a neighbour, with byte stores of this frame's bytes only.
+// No load sits between two stores, so nothing here is a latency chain.
+__device__ __forceinline__ void edge_chunk(const FrameRec& R, uint64_t p, uint8_t* __restrict__ wire)
 {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t lo = (R.off & ~uint64_t(15)) + k * PIECE;
-    if (lo >= R.end)
-        return;   // piece counts are an upper bound
-    const uint64_t hi = min(lo + PIECE, R.end);
     const uintptr_t sbase = reinterpret_cast<uintptr_t>(R.src) - R.data_w;   // source of wire byte q: sbase + q
-    const uint32_t s = uint32_t((sbase + lo) & 15u);                        // uniform: lo, p are 16-aligned
-    const uint32_t kw = key_rot(R.key, uint32_t(lo - R.pw));                 // uniform phase (mod 4)
-    bool data[EU];
-    v4u a[EU], b[EU];
+    const uintptr_t src_lo = reinterpret_cast<uintptr_t>(R.src);
+    const uintptr_t src_hi = src_lo + (R.end - R.data_w);
+    const uintptr_t a = sbase + p;
+    const uint32_t s = uint32_t(a & 15u);
+    const uintptr_t a0 = a - s;
+    v4u lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
+    if (a0 < src_hi && a0 + 16 > src_lo)
+        lo = ld16(reinterpret_cast<const uint8_t*>(a0));
+    if (s != 0 && a0 + 16 < src_hi && a0 + 32 > src_lo)
+        hi = ld16(reinterpret_cast<const uint8_t*>(a0 + 16));
+    const v4u d = s ? funnel(lo, hi, s) : lo;   // byte j: source byte of wire byte p + j
+    v4u w = {0, 0, 0, 0};
+    uint32_t own = 0;
 #pragma unroll
-    for (int u = 0; u < EU; ++u) {
-        const uint64_t p = lo + (uint64_t(u) * 64 + lane) * CHUNK;
-        data[u] = p < hi && p >= R.data_w && p + CHUNK <= R.end;
-        const uint8_t* a0 = reinterpret_cast<const uint8_t*>(sbase + p - s);
-        a[u] = data[u] ? (NT ? ld16nt(a0) : ld16(a0)) : v4u{0, 0, 0, 0};
+    for (uint32_t j = 0; j < CHUNK; ++j) {
+        const uint64_t q = p + j;
+        if (q < R.off || q >= R.end)
+            continue;
+        own |= 1u << j;
+        uint32_t b;
+        if (q >= R.data_w) {
+            b = lane_byte(d, j) ^ key_byte(R.key, q - R.pw);
+        } else {
+            const uint64_t r = q - R.off;
+            if (r < R.hdr) {
+                b = header_byte(R.opcode, R.mask, R.body, R.key, uint32_t(r));
+            } else {
+                const uint64_t k = r - R.hdr;   // close-status byte 0 or 1
+                b = uint32_t((k == 0 ? (R.status >> 8) : R.status) & 0xFF) ^ key_byte(R.key, k);
+            }
+        }
+        put_byte(w, j, b);
     }
-    if (s != 0) {
+    if (own == 0xFFFFu) {
+        st16nt(wire + p, w);
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < CHUNK; ++j)
+            if ((own >> j) & 1u)
+                wire[p + j] = uint8_t(lane_byte(w, j));
+    }
+}
+
+// One wave's piece k of frame R, in two phases so that a wave can keep two
+// pieces' loads in flight before storing either (load(), then store()).
+template <bool NT>
+struct Piece {
+    FrameRec R;
+    uint64_t lo = 0, hi = 0;
+    uintptr_t sbase = 0;   // source of wire byte q: sbase + q
+    uint32_t s = 0;        // source misalignment, uniform over the piece
+    uint32_t kw = 0;       // key rotated to the piece's phase (uniform)
+    bool live = false;
+    uint32_t dmask = 0;   // bit u: chunk u of this lane is all data (a bool array would land in LDS)
+    v4u a[EU], b[EU];
+
+    __device__ __forceinline__ void load(const FrameRec& rec, uint64_t k, bool exists)
+    {
+        R = rec;
+        const uint32_t lane = threadIdx.x & 63;
+        lo = (R.off & ~uint64_t(15)) + k * PIECE;
+        live = exists && lo < R.end;   // piece counts are an upper bound
+        hi = min(lo + PIECE, R.end);
+        sbase = reinterpret_cast<uintptr_t>(R.src) - R.data_w;
+        s = (WSG_DIAG_ENC & 2) ? 0u : uint32_t((sbase + lo) & 15u);
+        kw = key_rot(R.key, uint32_t(lo - R.pw));
+#pragma unroll
+        for (int u = 0; u < EU; ++u) {
+            const uint64_t p = lo + (uint64_t(u) * 64 + lane) * CHUNK;
+            const bool d = live && p < hi && p >= R.data_w && p + CHUNK <= R.end;
+            dmask |= uint32_t(d) << u;
+            const uint8_t* a0 = reinterpret_cast<const uint8_t*>(sbase + p - s);
+            a[u] = d ? (NT ? ld16nt(a0) : ld16(a0)) : v4u{0, 0, 0, 0};
+        }
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
             const uint64_t p = lo + (uint64_t(u) * 64 + lane) * CHUNK;
             const uint8_t* a0 = reinterpret_cast<const uint8_t*>(sbase + p - s);
-            b[u] = data[u] ? (NT ? ld16nt(a0 + CHUNK) : ld16(a0 + CHUNK)) : v4u{0, 0, 0, 0};
+            b[u] = ((dmask >> u) & 1u) && s ? ((NT && WSG_ENC_NT_HI) ? ld16nt(a0 + CHUNK) : ld16(a0 + CHUNK))
+                                          : v4u{0, 0, 0, 0};
         }
     }
+
+    __device__ __forceinline__ void store(uint8_t* __restrict__ wire) const
+    {
+        if (!live)
+            return;
+        const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
-    for (int u = 0; u < EU; ++u) {
-        const uint64_t p = lo + (uint64_t(u) * 64 + lane) * CHUNK;
-        if (data[u]) {
-            st16nt(wire + p, (s ? funnel(a[u], b[u], s) : a[u]) ^ kw);
-        } else if (p < hi) {
-            // header / status bytes, or an edge chunk shared with a neighbour
-            const uint64_t qlo = max(p, R.off), qhi = min(p + CHUNK, R.end);
-            if (qlo == p && qhi == p + CHUNK) {
-                v4u w = {0, 0, 0, 0};
-                for (uint32_t j = 0; j < CHUNK; ++j)
-                    put_byte(w, j, frame_byte(R, p + j));
-                st16nt(wire + p, w);
-            } else {
-                for (uint64_t q = qlo; q < qhi; ++q)
-                    wire[q] = uint8_t(frame_byte(R, q));
+        for (int u = 0; u < EU; ++u) {
+            const uint64_t p = lo + (uint64_t(u) * 64 + lane) * CHUNK;
+            if ((dmask >> u) & 1u) {
+                st16nt(wire + p, (s ? funnel(a[u], b[u], s) : a[u]) ^ kw);
+            } else if (p < hi && !(WSG_DIAG_ENC & 1)) {
+                edge_chunk(R, p, wire);   // header / status bytes, or a chunk shared with a neighbour
             }
         }
     }
-}
+};
 
 __device__ __forceinline__ uint64_t pieces_of(uint64_t frame_bytes) { return (frame_bytes + 15 + PIECE - 1) / PIECE; }
 
@@ -680,11 +803,40 @@ __global__ __launch_bounds__(BLOCK) void k_encode_mask(const uint8_t* __restrict
         return;   // capacity error latched by k_encode_finalize
     const uint32_t pieces = piece_start[n];
     const uint32_t waves = gridDim.x * (BLOCK / 64);
-    for (uint32_t q = blockIdx.x * (BLOCK / 64) + wave_id(); q < pieces; q += waves) {
-        const uint32_t i = piece_frame[q];
-        const wsg_send_desc d = desc[i];
-        const FrameRec R = make_rec(wire_off[i], payload + d.src_off, d.len, d.key, d.status, d.opcode, d.mask != 0);
-        encode_piece<true>(R, q - piece_start[i], wire);
+    // Software pipeline over the wave's pieces: while piece q streams, the
+    // descriptor of piece q + W (frame index already known) and the frame
+    // index of piece q + 2W are in flight, so the dependent metadata loads
+    // never sit between a piece's data loads and the previous piece's stores.
+    struct Meta {
+        Desc d;
+        uint64_t off;
+        uint32_t ps;
+    };
+    auto meta = [&](uint32_t i) { return Meta{load_desc(desc + i), wire_off[i], piece_start[i]}; };
+    uint32_t q = blockIdx.x * (BLOCK / 64) + wave_id();
+    if (q >= pieces)
+        return;
+    Meta cur = meta(piece_frame[q]);
+    uint32_t i_next = (q + waves < pieces) ? piece_frame[q + waves] : 0;
+    for (;;) {
+        Piece<WSG_ENC_NT_SRC != 0> pc;
+        pc.load(make_rec(cur.off, payload + cur.d.src_off, cur.d.len, cur.d.key, cur.d.status, cur.d.opcode,
+                         cur.d.mask),
+                q - cur.ps, true);
+        const uint32_t qn = q + waves;
+        const bool more = qn < pieces;
+        Meta nxt = cur;
+        uint32_t i_after = 0;
+        if (more) {
+            nxt = meta(i_next);
+            i_after = (qn + waves < pieces) ? piece_frame[qn + waves] : 0;
+        }
+        pc.store(wire);
+        if (!more)
+            break;
+        cur = nxt;
+        i_next = i_after;
+        q = qn;
     }
 }
 
@@ -699,9 +851,11 @@ __global__ __launch_bounds__(BLOCK) void k_fanout(const uint8_t* __restrict__ pa
     const uint64_t pieces = uint64_t(per_frame) * k;
     const uint64_t waves = uint64_t(gridDim.x) * (BLOCK / 64);
     for (uint64_t q = uint64_t(blockIdx.x) * (BLOCK / 64) + wave_id(); q < pieces; q += waves) {
+        Piece<false> pc;
         const uint32_t i = uint32_t(q / per_frame);
-        const FrameRec R = make_rec(uint64_t(i) * fsize, payload, len, keys[i], 0, opcode, mask != 0);
-        encode_piece<false>(R, q - uint64_t(i) * per_frame, wire);
+        pc.load(make_rec(uint64_t(i) * fsize, payload, len, keys[i], 0, opcode, mask != 0),
+                q - uint64_t(i) * per_frame, true);
+        pc.store(wire);
     }
 }
 

@@ -79,18 +79,16 @@ def c4_fanout(length=4096, k=10000, seed=4):
 
 
 def c5_rank_frames(rank, world, n_total=1 << 20, chunk=1024):
-    """Frame indices owned by `rank` when chunks of `chunk` frames are dealt
-    round-robin over `world` ranks."""
-    n_chunks = (n_total + chunk - 1) // chunk
-    mine = np.arange(rank, n_chunks, world, dtype=np.int64)
-    idx = (mine[:, None] * chunk + np.arange(chunk, dtype=np.int64)[None, :]).reshape(-1)
-    return idx[idx < n_total]
+    """Frame indices owned by `rank` (chunks dealt round-robin, shard.py)."""
+    from .shard import rank_frames
+
+    return rank_frames(rank, world, n_total, chunk)
 
 
 def c5_shard(rank, world, n_total=1 << 20, size=16384, chunk=1024, seed=5, max_frames=None):
-    """This rank's encode batch: (payload, desc, frame_ids).  Every frame's
-    payload and key derive from its global index, so shards are disjoint and
-    the union over ranks is the same 1 Mi-frame job at any world size."""
+    """This rank's encode batch: (payload, desc, frame_ids).  Keys derive from
+    the global frame index (shards are disjoint, the key set is the same job
+    at any world size); payload bytes are seeded per shard."""
     ids = c5_rank_frames(rank, world, n_total, chunk)
     if max_frames is not None:
         ids = ids[:max_frames]

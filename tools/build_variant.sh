@@ -1,0 +1,17 @@
+#!/bin/bash
+# Build an A/B variant of libwsg.so with extra -D flags into cppserver_amd/_build/var/<name>/.
+#   tools/build_variant.sh NAME [-DFOO=1 ...]
+set -e
+name=$1; shift
+root=$(cd "$(dirname "$0")/.." && pwd)
+out=$root/cppserver_amd/_build/var/$name
+mkdir -p "$out"
+cd "$out"
+H=/opt/rocm/bin/hipcc
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$root/include $*"
+$H $F -c $root/cppserver_amd/csrc/wsg_kernels.hip -o k.o
+$H $F -c $root/cppserver_amd/csrc/wsg_capi.hip -o c.o
+$H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws.cpp -o w.o
+$H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws_api.cpp -o a.o
+$H --offload-arch=gfx950 -shared -o libwsg.so k.o c.o w.o a.o
+echo "$out/libwsg.so"

@@ -50,6 +50,50 @@ __global__ __launch_bounds__(BLOCK) void k_stream(const u32x4* __restrict__ src,
     }
 }
 
+// Pattern of the encode kernel: each WAVE owns a contiguous piece of
+// 64 x 16 x U bytes; pieces are dealt round-robin over all waves.
+template <int BLOCK, int U, int NT>
+__global__ __launch_bounds__(BLOCK) void k_wavepiece(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                     uint64_t n16, uint32_t key)
+{
+    const uint64_t per_piece = uint64_t(64) * U;
+    const uint64_t pieces = n16 / per_piece;
+    const uint64_t waves = uint64_t(gridDim.x) * (BLOCK / 64);
+    const uint64_t lane = threadIdx.x & 63;
+    for (uint64_t q = uint64_t(blockIdx.x) * (BLOCK / 64) + (threadIdx.x >> 6); q < pieces; q += waves) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            v[u] = __builtin_nontemporal_load(src + q * per_piece + u * 64 + lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_nontemporal_store(v[u] ^ key, dst + q * per_piece + u * 64 + lane);
+    }
+}
+
+template <int BLOCK, int U>
+void run_wp(const char* name, const u32x4* src, u32x4* dst, uint64_t n16, int cus, int bpc)
+{
+    const uint64_t pieces = n16 / (64 * U);
+    const int grid = int(std::min<uint64_t>(pieces / (BLOCK / 64), uint64_t(cus) * bpc));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i)
+        k_wavepiece<BLOCK, U, 3><<<grid, BLOCK>>>(src, dst, n16, 0x12345678u);
+    const int reps = 20;
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i)
+        k_wavepiece<BLOCK, U, 3><<<grid, BLOCK>>>(src, dst, n16, 0x12345678u);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    ms /= reps;
+    printf("%-34s block=%4d U=%2d bpc=%2d grid=%6d  %8.1f us  %7.1f GB/s\n", name, BLOCK, U, bpc, grid, ms * 1e3,
+           2.0 * n16 * 16 / (ms * 1e-3) / 1e9);
+}
+
 template <int BLOCK, int U, int NT>
 void run(const char* name, const u32x4* src, u32x4* dst, uint64_t n16, int cus, int bpc)
 {
@@ -90,6 +134,18 @@ int main(int argc, char** argv)
     CK(hipMalloc(&dst, bytes));
     CK(hipMemset(src, 1, bytes));
     CK(hipMemset(dst, 0, bytes));
+    if (argc > 2 && std::string(argv[2]) == "pattern") {
+        // block tiles (decode) vs wave pieces (encode), both nontemporal
+        for (int rep = 0; rep < 2; ++rep) {
+            run<256, 4, 3>("block-tile 16K", src, dst, n16, cus, 32);
+            run_wp<256, 4>("wave-piece 4K", src, dst, n16, cus, 32);
+            run_wp<256, 8>("wave-piece 8K", src, dst, n16, cus, 16);
+            run_wp<256, 16>("wave-piece 16K", src, dst, n16, cus, 8);
+        }
+        CK(hipFree(src));
+        CK(hipFree(dst));
+        return 0;
+    }
     if (argc > 2 && std::string(argv[2]) == "calib") {
         // PMC calibration: known bytes (read n16*16, write n16*16 per launch)
         run<256, 4, 0>("calib plain", src, dst, n16, cus, 8);

@@ -20,11 +20,21 @@ def main():
     # settings: "BPC" or "BPC@path/to/libwsg.so"
     settings = sys.argv[1:] or ["8", "16", "32"]
     n, size = int(os.environ.get("FRAMES", 4096)), int(os.environ.get("SIZE", 65536))
+    # ROT distinct batches, used in turn, so no step finds its input in the
+    # 256 MiB Infinity Cache left warm by the previous step
+    rot = int(os.environ.get("ROT", 1))
     wire, fs, _ = wl.c2_wire(n, size, seed=1)
-    w = torch.from_numpy(wire).cuda()
+    ws = [torch.from_numpy(wire).cuda()] + [torch.from_numpy(wl.c2_wire(n, size, seed=2 + r)[0]).cuda()
+                                           for r in range(rot - 1)]
     f = torch.from_numpy(fs.view(np.int64)).cuda()
-    out = torch.empty_like(w)
+    outs = [torch.empty_like(ws[0]) for _ in range(rot)]
     info = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    it = [0]
+
+    def step1(c):
+        k = it[0] % rot
+        it[0] += 1
+        c.decode_batch(ws[k], f, out=outs[k], info=info)
     codecs = {}
     for b in settings:
         bpc, _, path = b.partition("@")
@@ -39,10 +49,10 @@ def main():
         for b in settings:
             c = codecs[b]
             for _ in range(3):
-                c.decode_batch(w, f, out=out, info=info)
+                step1(c)
             e0.record()
             for _ in range(20):
-                c.decode_batch(w, f, out=out, info=info)
+                step1(c)
             e1.record()
             e1.synchronize()
             bare[b].append(e0.elapsed_time(e1) / 20)
@@ -50,7 +60,7 @@ def main():
             c.timing_read()
             e0.record()
             for _ in range(20):
-                c.decode_batch(w, f, out=out, info=info)
+                step1(c)
             e1.record()
             e1.synchronize()
             ms, k = c.timing_read()
@@ -58,6 +68,7 @@ def main():
             kern[b].append(ms / k)
             step[b].append(e0.elapsed_time(e1) / 20)
     alg = 2 * len(wire)
+    print("batches in rotation: %d x %.0f MB wire" % (rot, len(wire) / 1e6))
     for b in settings:
         km, sm, bm = statistics.median(kern[b]), statistics.median(step[b]), statistics.median(bare[b])
         print("%-40s kernel %.4f ms (%.0f GB/s)  step %.4f ms (%.0f GiB/s)  untimed step %.4f ms (%.0f GiB/s)  spread %.1f%%" % (

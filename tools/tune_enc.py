@@ -1,0 +1,53 @@
+"""Interleaved A/B timing of encode variants (libwsg.so builds) on C5/C3-like batches.
+
+usage: CFG=c5|c3 python tools/tune_enc.py path/to/libwsg.so ...
+"""
+import os
+import statistics
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import cppserver_amd as ca  # noqa: E402
+from cppserver_amd import workloads as wl  # noqa: E402
+
+
+def main():
+    libs = sys.argv[1:] or [None]
+    cfg = os.environ.get("CFG", "c5")
+    if cfg == "c5":
+        payload, desc, _ = wl.c5_shard(0, 8, n_total=1 << 20)      # one rank's share of 8: 131072 x 16 KiB
+    else:
+        payload, desc = wl.c3_batch(16384, 128, 65536, seed=3)
+    cap = int(sum(ca.frame_size(int(d["opcode"]), bool(d["mask"]), int(d["len"])) for d in desc[:1])) * 0
+    cap = int(np.sum([ca.frame_size(0x82, True, int(x)) for x in desc["len"]]))
+    n = len(desc)
+    p = [torch.from_numpy(payload).cuda() for _ in range(2)]
+    d = ca.desc_to_tensor(desc, "cuda")
+    wires = [torch.empty(cap, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    woff = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    codecs = [ca.Codec(0, lib_path=l) for l in libs]
+    kern = [[] for _ in libs]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for rep in range(int(os.environ.get("REPS", 5))):
+        for ci, c in enumerate(codecs):
+            for it in range(3):
+                c.encode_batch(p[it & 1], d, wire=wires[it & 1], wire_cap=cap, wire_off=woff)
+            c.timing(True, 1)
+            c.timing_read()
+            for it in range(8):
+                c.encode_batch(p[it & 1], d, wire=wires[it & 1], wire_cap=cap, wire_off=woff)
+            ms, k = c.timing_read()
+            c.timing(False)
+            kern[ci].append(ms / k)
+    alg = len(payload) + cap
+    for l, k in zip(libs, kern):
+        m = statistics.median(k)
+        print("%-50s encode kernel %.4f ms  %.0f GB/s  spread %.1f%%" % (l, m, alg / m / 1e6,
+                                                                       100 * (max(k) - min(k)) / m))
+
+
+if __name__ == "__main__":
+    main()
