@@ -62,6 +62,8 @@ def lib(path=None):
         "wsg_fanout_encode": (ci, [vp, vp, u64, vp, u32, ctypes.c_uint8, ci, vp, u64, vp]),
         "wsg_xor_host": (ci, [vp, vp, vp, sz, u32, u32]),
         "wsg_decode_batch_host": (ci, [vp, vp, u64, vp, u32, vp, vp]),
+        "wsg_host_alloc": (ci, [sz, ctypes.POINTER(vp)]),
+        "wsg_host_free": (ci, [vp]),
         "wsg_frame_size": (u64, [ctypes.c_uint8, ci, u64, i32]),
         "wsg_header_pack": (ci, [ctypes.c_uint8, ci, u64, i32, u32, vp]),
         "wsg_header_unpack": (ci, [vp, u64, vp]),
@@ -107,6 +109,27 @@ def header_unpack(data):
     info = np.zeros(1, dtype=RECV_INFO)
     rc = lib().wsg_header_unpack(data, len(data), _np_ptr(info))
     return rc, info[0]
+
+
+class _Pinned:
+    """Owner of a wsg_host_alloc block; freed when the last view dies."""
+
+    def __init__(self, nbytes):
+        self.ptr = ctypes.c_void_p()
+        _check(lib().wsg_host_alloc(nbytes, ctypes.byref(self.ptr)), "wsg_host_alloc")
+
+    def __del__(self):
+        if self.ptr:
+            lib().wsg_host_free(self.ptr)
+            self.ptr = None
+
+
+def pinned_empty(nbytes, dtype=np.uint8):
+    """numpy array in page-locked host memory (DMA without staging)."""
+    owner = _Pinned(max(int(nbytes), 1))
+    buf = (ctypes.c_uint8 * max(int(nbytes), 1)).from_address(owner.ptr.value)
+    buf._owner = owner   # the numpy view keeps buf alive, buf keeps the block alive
+    return np.frombuffer(buf, dtype=np.uint8)[: int(nbytes)].view(dtype)
 
 
 def abi_frame_size(opcode, mask, length, status=0):
@@ -207,10 +230,11 @@ class Codec:
         _check(self._L.wsg_xor_host(self._ctx, src, dst, len(src), key, phase), "wsg_xor_host")
         return dst.raw[: len(src)]
 
-    def decode_batch_host(self, wire, frame_start):
+    def decode_batch_host(self, wire, frame_start, out=None):
         wire = np.ascontiguousarray(wire, dtype=np.uint8)
         fs = np.ascontiguousarray(frame_start, dtype=np.uint64)
-        out = np.empty(max(len(wire), 1), dtype=np.uint8)
+        if out is None:
+            out = np.empty(max(len(wire), 1), dtype=np.uint8)
         info = np.zeros(max(len(fs), 1), dtype=RECV_INFO)
         rc = self._L.wsg_decode_batch_host(self._ctx, _np_ptr(wire), len(wire), _np_ptr(fs), len(fs),
                                            _np_ptr(out), _np_ptr(info))

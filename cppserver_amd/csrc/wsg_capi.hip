@@ -32,6 +32,32 @@ struct wsg_ctx {
     uint64_t* d_fs = nullptr;
     wsg_recv_info* d_info = nullptr;
     uint64_t fs_cap = 0;
+    // pipelined host path (wsg_decode_batch_host): one stream + staging per slot
+    struct Slot {
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;
+        uint8_t* d_wire = nullptr;       // segment, decoded in place
+        uint64_t wire_cap = 0;
+        uint8_t* h_in = nullptr;         // pinned staging for pageable callers
+        uint8_t* h_out = nullptr;
+        uint64_t host_cap = 0;
+        uint64_t* h_fs = nullptr;        // rebased frame starts (pinned)
+        wsg_recv_info* h_info = nullptr; // info staging (pinned)
+        uint64_t* d_fs = nullptr;
+        wsg_recv_info* d_info = nullptr;
+        uint64_t frames_cap = 0;
+        uint32_t* d_tiles = nullptr;
+        uint64_t tiles_cap = 0;
+        // work to finish on the host once `done` has fired
+        bool busy = false;
+        uint8_t* out_dst = nullptr;      // pageable destination of h_out (null: DMA'd directly)
+        uint64_t out_src = 0, out_len = 0;
+        wsg_recv_info* info_dst = nullptr;
+        uint32_t info_n = 0;
+        uint64_t base = 0;               // wire offset of the segment's first byte
+    };
+    static constexpr int kSlots = 3;
+    Slot slots[kSlots];
     // timing of the dominant kernel
     struct EvPair {
         hipEvent_t a, b;
@@ -268,6 +294,26 @@ int wsg_destroy(wsg_ctx* c)
     (void)hipFree(c->d_info);
     if (c->h_stage)
         (void)hipHostFree(c->h_stage);
+    for (auto& sl : c->slots) {
+        if (sl.stream)
+            (void)hipStreamSynchronize(sl.stream);
+        (void)hipFree(sl.d_wire);
+        (void)hipFree(sl.d_tiles);
+        (void)hipFree(sl.d_fs);
+        (void)hipFree(sl.d_info);
+        if (sl.h_in)
+            (void)hipHostFree(sl.h_in);
+        if (sl.h_out)
+            (void)hipHostFree(sl.h_out);
+        if (sl.h_fs)
+            (void)hipHostFree(sl.h_fs);
+        if (sl.h_info)
+            (void)hipHostFree(sl.h_info);
+        if (sl.done)
+            (void)hipEventDestroy(sl.done);
+        if (sl.stream)
+            (void)hipStreamDestroy(sl.stream);
+    }
     if (c->stream)
         (void)hipStreamDestroy(c->stream);
     delete c;
@@ -291,6 +337,31 @@ int wsg_sync(wsg_ctx* c, void* stream)
     return -int(e & 0xFFu);
 }
 
+namespace {
+
+// Device decode with explicit tile-map scratch (the pipelined host path runs
+// several of these concurrently, one per slot stream).
+int decode_launch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const uint64_t* d_frame_start, uint32_t n,
+                  uint8_t* d_out, wsg_recv_info* d_info, uint32_t* d_tiles, hipStream_t s)
+{
+    if (n == 0) {
+        if (wire_len && d_out != d_wire)
+            WSG_HIP(hipMemcpyAsync(d_out, d_wire, wire_len, hipMemcpyDeviceToDevice, s));
+        return WSG_OK;
+    }
+    const uint64_t tiles = ceil_div(wire_len, wsg::TILE);
+    WSG_HIP(wsg::launch_decode_parse(s, d_wire, wire_len, d_frame_start, n, d_info, d_tiles, tiles, c->d_err));
+    if (tiles == 0)
+        return WSG_OK;
+    const int t = timing_begin(c, s);
+    WSG_HIP(wsg::launch_decode_unmask(s, grid_for(c, tiles), d_wire, d_out, wire_len, d_frame_start, d_info, n,
+                                      d_tiles, tiles));
+    timing_end(c, s, t);
+    return WSG_OK;
+}
+
+} // namespace
+
 int wsg_decode_batch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const uint64_t* d_frame_start, uint32_t n,
                      uint8_t* d_out, wsg_recv_info* d_info, void* stream)
 {
@@ -298,23 +369,9 @@ int wsg_decode_batch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const
         return WSG_EINVAL;
     if (!aligned16(d_wire) || !aligned16(d_out))
         return WSG_EINVAL;
-    hipStream_t s = pick(c, stream);
-    if (n == 0) {
-        if (wire_len && d_out != d_wire)
-            WSG_HIP(hipMemcpyAsync(d_out, d_wire, wire_len, hipMemcpyDeviceToDevice, s));
-        return WSG_OK;
-    }
-    const uint64_t tiles = ceil_div(wire_len, wsg::TILE);
-    if (int rc = ensure_tiles(c, tiles))
+    if (int rc = ensure_tiles(c, ceil_div(wire_len, wsg::TILE)))
         return rc;
-    WSG_HIP(wsg::launch_decode_parse(s, d_wire, wire_len, d_frame_start, n, d_info, c->d_tiles, tiles, c->d_err));
-    if (tiles == 0)
-        return WSG_OK;
-    const int t = timing_begin(c, s);
-    WSG_HIP(wsg::launch_decode_unmask(s, grid_for(c, tiles), d_wire, d_out, wire_len, d_frame_start, d_info, n,
-                                      c->d_tiles, tiles));
-    timing_end(c, s, t);
-    return WSG_OK;
+    return decode_launch(c, d_wire, wire_len, d_frame_start, n, d_out, d_info, c->d_tiles, pick(c, stream));
 }
 
 int wsg_encode_batch(wsg_ctx* c, const uint8_t* d_payload, const wsg_send_desc* d_desc, uint32_t n, uint8_t* d_wire,
@@ -388,23 +445,199 @@ int wsg_xor_host(wsg_ctx* c, const void* src, void* dst, size_t len, uint32_t ke
     return WSG_OK;
 }
 
+namespace {
+
+bool host_pinned(const void* p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+int slot_reserve(wsg_ctx::Slot& sl, uint64_t bytes, uint64_t frames, bool need_host)
+{
+    if (!sl.stream) {
+        WSG_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+        WSG_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    }
+    if (int rc = ensure_array(sl.d_wire, sl.wire_cap, bytes + 32))
+        return rc;
+    if (int rc = ensure_array(sl.d_tiles, sl.tiles_cap, ceil_div(bytes + 32, wsg::TILE)))
+        return rc;
+    if (frames > sl.frames_cap) {
+        (void)hipFree(sl.d_fs);
+        (void)hipFree(sl.d_info);
+        if (sl.h_fs)
+            (void)hipHostFree(sl.h_fs);
+        if (sl.h_info)
+            (void)hipHostFree(sl.h_info);
+        sl.d_fs = nullptr;
+        sl.d_info = nullptr;
+        sl.h_fs = nullptr;
+        sl.h_info = nullptr;
+        sl.frames_cap = 0;
+        if (hipMalloc(&sl.d_fs, frames * sizeof(uint64_t)) != hipSuccess ||
+            hipMalloc(&sl.d_info, frames * sizeof(wsg_recv_info)) != hipSuccess ||
+            hipHostMalloc(&sl.h_fs, frames * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(&sl.h_info, frames * sizeof(wsg_recv_info), hipHostMallocDefault) != hipSuccess)
+            return WSG_ENOMEM;
+        sl.frames_cap = frames;
+    }
+    if (need_host && bytes + 32 > sl.host_cap) {
+        if (sl.h_in)
+            (void)hipHostFree(sl.h_in);
+        if (sl.h_out)
+            (void)hipHostFree(sl.h_out);
+        sl.h_in = sl.h_out = nullptr;
+        sl.host_cap = 0;
+        if (hipHostMalloc(&sl.h_in, bytes + 32, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(&sl.h_out, bytes + 32, hipHostMallocDefault) != hipSuccess)
+            return WSG_ENOMEM;
+        sl.host_cap = bytes + 32;
+    }
+    return WSG_OK;
+}
+
+// Wait for a slot's previous segment and finish its host-side copies.
+int slot_drain(wsg_ctx::Slot& sl)
+{
+    if (!sl.busy)
+        return WSG_OK;
+    WSG_HIP(hipEventSynchronize(sl.done));
+    if (sl.out_dst && sl.out_len)
+        std::memcpy(sl.out_dst, sl.h_out + sl.out_src, sl.out_len);
+    for (uint32_t k = 0; k < sl.info_n; ++k) {
+        wsg_recv_info r = sl.h_info[k];
+        r.payload_off += sl.base;   // segment-relative -> wire offset
+        sl.info_dst[k] = r;
+    }
+    sl.busy = false;
+    return WSG_OK;
+}
+
+} // namespace
+
+int wsg_host_alloc(size_t bytes, void** out)
+{
+    if (!out)
+        return WSG_EINVAL;
+    *out = nullptr;
+    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+        return WSG_ENOMEM;
+    return WSG_OK;
+}
+
+int wsg_host_free(void* p)
+{
+    if (p && hipHostFree(p) != hipSuccess)
+        return WSG_EHIP;
+    return WSG_OK;
+}
+
 int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start,
                           uint32_t n, uint8_t* out, wsg_recv_info* info)
 {
     if (!c || (wire_len && (!wire || !out)) || (n && (!frame_start || !info)))
         return WSG_EINVAL;
-    if (int rc = ensure_stage(c, wire_len, n))
-        return rc;
-    hipStream_t s = c->stream;
-    WSG_HIP(hipMemcpyAsync(c->d_stage, wire, wire_len, hipMemcpyHostToDevice, s));
-    if (n)
-        WSG_HIP(hipMemcpyAsync(c->d_fs, frame_start, n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    if (int rc = wsg_decode_batch(c, c->d_stage, wire_len, c->d_fs, n, c->d_stage, c->d_info, s))
-        return rc;
-    WSG_HIP(hipMemcpyAsync(out, c->d_stage, wire_len, hipMemcpyDeviceToHost, s));
-    if (n)
-        WSG_HIP(hipMemcpyAsync(info, c->d_info, n * sizeof(wsg_recv_info), hipMemcpyDeviceToHost, s));
-    return wsg_sync(c, s);
+    if (n == 0) {
+        if (wire_len && out != wire)
+            std::memmove(out, wire, wire_len);
+        return WSG_OK;
+    }
+    uint64_t seg_bytes = 32ull << 20;
+    if (const char* e = std::getenv("WSG_STAGE_MB"))
+        seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+    const bool in_pinned = host_pinned(wire), out_pinned = host_pinned(out);
+
+    // segments: runs of whole frames of about seg_bytes; segment k covers wire
+    // bytes [start of its first frame, start of the next segment's first frame)
+    std::vector<uint32_t> cut{0};
+    {
+        uint64_t from = 0;
+        for (uint32_t i = 1; i < n; ++i) {
+            if (frame_start[i] >= wire_len)
+                break;   // frames past the wire: error frames, kept with the last segment
+            if (frame_start[i] > from && frame_start[i] - from >= seg_bytes) {
+                cut.push_back(i);
+                from = frame_start[i];
+            }
+        }
+        cut.push_back(n);
+    }
+    const size_t nseg = cut.size() - 1;
+    uint64_t max_bytes = 0, max_frames = 0;
+    auto seg_lo = [&](size_t k) { return k == 0 ? uint64_t(0) : std::min(frame_start[cut[k]], wire_len); };
+    auto seg_hi = [&](size_t k) { return k + 1 == nseg ? wire_len : std::min(frame_start[cut[k + 1]], wire_len); };
+    for (size_t k = 0; k < nseg; ++k) {
+        const uint64_t base = seg_lo(k) & ~uint64_t(15);
+        max_bytes = std::max(max_bytes, std::max(seg_hi(k), seg_lo(k)) - base);
+        max_frames = std::max<uint64_t>(max_frames, cut[k + 1] - cut[k]);
+    }
+    for (auto& sl : c->slots)
+        if (int rc = slot_reserve(sl, max_bytes, max_frames, !in_pinned || !out_pinned))
+            return rc;
+
+    for (size_t k = 0; k < nseg; ++k) {
+        wsg_ctx::Slot& sl = c->slots[k % wsg_ctx::kSlots];
+        if (int rc = slot_drain(sl))
+            return rc;
+        const uint32_t i0 = cut[k], i1 = cut[k + 1], m = i1 - i0;
+        const uint64_t lo = seg_lo(k), hi = std::max(seg_hi(k), lo);
+        const uint64_t base = lo & ~uint64_t(15);   // 16-B aligned device copy of [base, hi)
+        const uint64_t len = hi - base;
+        for (uint32_t j = 0; j < m; ++j)
+            sl.h_fs[j] = frame_start[i0 + j] >= base ? frame_start[i0 + j] - base : ~uint64_t(0);
+        const uint8_t* src = wire + base;
+        if (!in_pinned) {
+            std::memcpy(sl.h_in, wire + base, len);
+            src = sl.h_in;
+        }
+        WSG_HIP(hipMemcpyAsync(sl.d_wire, src, len, hipMemcpyHostToDevice, sl.stream));
+        WSG_HIP(hipMemcpyAsync(sl.d_fs, sl.h_fs, m * sizeof(uint64_t), hipMemcpyHostToDevice, sl.stream));
+        if (int rc = decode_launch(c, sl.d_wire, len, sl.d_fs, m, sl.d_wire, sl.d_info, sl.d_tiles, sl.stream))
+            return rc;
+        // copy back [lo, hi): bytes before lo belong to the previous segment
+        const uint64_t back = hi - lo;
+        if (out_pinned) {
+            WSG_HIP(hipMemcpyAsync(out + lo, sl.d_wire + (lo - base), back, hipMemcpyDeviceToHost, sl.stream));
+            sl.out_dst = nullptr;
+        } else {
+            WSG_HIP(hipMemcpyAsync(sl.h_out, sl.d_wire + (lo - base), back, hipMemcpyDeviceToHost, sl.stream));
+            sl.out_dst = out + lo;
+            sl.out_src = 0;
+        }
+        sl.out_len = back;
+        WSG_HIP(hipMemcpyAsync(sl.h_info, sl.d_info, m * sizeof(wsg_recv_info), hipMemcpyDeviceToHost, sl.stream));
+        sl.info_dst = info + i0;
+        sl.info_n = m;
+        sl.base = base;
+        WSG_HIP(hipEventRecord(sl.done, sl.stream));
+        sl.busy = true;
+    }
+    for (auto& sl : c->slots)
+        if (int rc = slot_drain(sl))
+            return rc;
+    (void)wsg_sync(c, nullptr);   // clear the latch: segment-relative indices are not meaningful here
+
+    // batch semantics: a frame that runs into the next segment's first frame
+    // overlaps it (EINVAL), it is not truncated; and the status is the error
+    // of the lowest-indexed bad frame
+    int first = WSG_OK;
+    for (uint32_t i = 0; i < n; ++i) {
+        wsg_recv_info& r = info[i];
+        if (r.error == WSG_ETRUNC && i + 1 < n && frame_start[i] < wire_len) {
+            wsg_recv_info h;
+            if (wsg_header_unpack(wire + frame_start[i], wire_len - frame_start[i], &h) == WSG_OK &&
+                h.len <= wire_len - frame_start[i] - h.hdr_len)
+                r.error = int8_t(WSG_EINVAL);
+        }
+        if (r.error && !first)
+            first = r.error;
+    }
+    return first;
 }
 
 uint64_t wsg_frame_size(uint8_t opcode, int mask, uint64_t len, int32_t status)

@@ -128,11 +128,19 @@ int wsg_fanout_encode(wsg_ctx* ctx, const uint8_t* d_payload, uint64_t len,
  * the GPU (H2D, kernel, D2H), synchronous.  src may equal dst.               */
 int wsg_xor_host(wsg_ctx* ctx, const void* src, void* dst, size_t len,
                  uint32_t key, uint32_t phase);
-/* Batch decode of a host wire buffer through pinned staging with copy/compute
- * overlap.  Same semantics as wsg_decode_batch, host pointers.                */
+/* Batch decode of a host wire buffer, synchronous, same results as
+ * wsg_decode_batch with host pointers (payload_off are wire offsets).  The
+ * batch is cut into ~32 MiB segments of whole frames ($WSG_STAGE_MB) that
+ * flow through three stream slots, so H2D of one segment, decode of the next
+ * and D2H of a third overlap.  Pinned buffers (wsg_host_alloc, or registered)
+ * are DMA'd directly; pageable ones are staged through pinned memory.        */
 int wsg_decode_batch_host(wsg_ctx* ctx, const uint8_t* wire, uint64_t wire_len,
                           const uint64_t* frame_start, uint32_t n,
                           uint8_t* out, wsg_recv_info* info);
+
+/* Page-locked host memory for receive/send buffers (DMA without staging). */
+int wsg_host_alloc(size_t bytes, void** out);
+int wsg_host_free(void* p);
 
 /* ---- single-frame header helpers (host; same code the kernels run) ------ */
 /* Total frame size PrepareSendFrame produces (ws.cpp:215-252).               */

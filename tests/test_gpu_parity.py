@@ -281,6 +281,36 @@ def test_decode_batch_host(codec):
         assert np.array_equal(info[f], info_o[f])
 
 
+@pytest.mark.parametrize("stage_mb", ["1", "32"])
+def test_decode_batch_host_segmented(codec, stage_mb, monkeypatch):
+    """The pipelined host path cuts the batch into segments; results must not
+    depend on where the cuts fall (ragged frames, misaligned segment starts,
+    a truncated last frame, an overlap at a segment edge)."""
+    monkeypatch.setenv("WSG_STAGE_MB", stage_mb)
+    rng = np.random.default_rng(int(stage_mb))
+    payload, desc = _mixed_desc(rng, 600, 0, 70000)
+    wire, off = oracle.encode_batch(payload, desc)
+    fs = off[:-1].copy()
+    for variant in ("ok", "trunc", "overlap"):
+        w, f = wire, fs
+        if variant == "trunc":
+            w = wire[:-5]
+        if variant == "overlap":
+            f = fs.copy()
+            f[300] = f[300] + 1     # frame 299 now overlaps frame 300
+        rc_o, out_o, info_o = oracle.decode_batch(w, f)
+        for pinned in (False, True):
+            src = w
+            if pinned:
+                src = ca.pinned_empty(len(w))
+                src[:] = w
+            rc, out, info = codec.decode_batch_host(src, f)
+            assert rc == rc_o, (variant, pinned)
+            assert np.array_equal(out, out_o), (variant, pinned)
+            for fld in INFO_FIELDS:
+                assert np.array_equal(info[fld], info_o[fld]), (variant, pinned, fld)
+
+
 def test_timing_hook_counts_launches(codec):
     wire, fs, _ = wl.c2_wire(64, 65536, seed=10)
     w, f = dev(wire), dev(fs.view(np.int64))
