@@ -333,7 +333,7 @@ def main():
     k_avg_ms = kernel_ms / max(launches, 1)
     k_avg_ms = max_over_ranks(k_avg_ms, world, device)
     achieved = w.alg_bytes / (k_avg_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(args.pmc, w.cfg)
+    traffic = pmc_traffic(args.pmc, w.cfg) if args.frames is None and args.size is None else None
 
     extras = {}
     if w.cfg == "c5" and world > 1:
@@ -356,7 +356,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": METRIC,
+            "metric": METRIC if w.cfg == "c2" else "WS payload GiB/s (device-resident), " + w.cfg.upper(),
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -368,8 +368,9 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded random payloads and keys)",
-            "config": dict({"workload": w.workload, "parallelism": "independent batch per GPU (dp%d)" % world},
-                           **w.extra),
+            "config": dict({"workload": w.workload,
+                            "parallelism": ("1 Mi-frame job split round-robin over %d GPUs" % world) if w.cfg == "c5"
+                            else "independent batch per GPU (dp%d)" % world}, **w.extra),
             "roofline": {
                 "bound": "hbm",
                 "kernel": w.kernel,
