@@ -74,6 +74,13 @@ def lib(path=None):
         "wsg_session_prepare_receive": (ci, [vp, vp, sz, vp, vp]),
         "wsg_session_required": (sz, [vp]),
         "wsg_session_clear": (ci, [vp]),
+        "wsg_rx_create": (ci, [vp, ctypes.POINTER(vp)]),
+        "wsg_rx_destroy": (ci, [vp]),
+        "wsg_rx_feed": (ci, [vp, vp, vp, sz]),
+        "wsg_rx_clear": (ci, [vp, vp]),
+        "wsg_rx_forget": (ci, [vp, vp]),
+        "wsg_rx_pending": (ci, [vp, ctypes.POINTER(u32), ctypes.POINTER(u64)]),
+        "wsg_rx_flush": (ci, [vp, vp, vp, ctypes.POINTER(u32)]),
         "wsg_timing_enable": (ci, [vp, ci]),
         "wsg_timing_read": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ci]),
     }
@@ -254,6 +261,8 @@ class Codec:
 
 RECEIVE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t,
                               ctypes.c_int)
+RX_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8),
+                         ctypes.c_size_t, ctypes.c_int)
 
 
 class Session:
@@ -309,6 +318,65 @@ class Session:
 
     def clear(self):
         _check(self._L.wsg_session_clear(self._s), "wsg_session_clear")
+
+
+class RxBatch:
+    """Batched receive over many sessions through the C-ABI (wsg_rx_*): feed()
+    frames each session's stream on the host, flush() unmasks the batch in one
+    GPU pass and fires every session's callbacks in arrival order.  Events are
+    (session, kind, payload bytes, status)."""
+
+    def __init__(self, codec):
+        self._L = lib()
+        self._codec = codec
+        rx = ctypes.c_void_p()
+        _check(self._L.wsg_rx_create(codec._ctx, ctypes.byref(rx)), "wsg_rx_create")
+        self._rx = rx
+        self._events = []
+        self._by_ptr = {}
+
+        def _cb(user, sess, kind, data, size, status):
+            self._events.append((self._by_ptr.get(sess), kind, ctypes.string_at(data, size) if size else b"",
+                                 status))
+
+        self._cb = RX_CB(_cb)
+
+    def close(self):
+        if getattr(self, "_rx", None):
+            self._L.wsg_rx_destroy(self._rx)
+            self._rx = None
+
+    __del__ = close
+
+    def _reg(self, session):
+        self._by_ptr[session._s.value] = session
+        return session._s
+
+    def feed(self, session, data):
+        buf = bytes(data)
+        _check(self._L.wsg_rx_feed(self._rx, self._reg(session), buf if buf else None, len(buf)), "wsg_rx_feed")
+
+    def clear(self, session):
+        _check(self._L.wsg_rx_clear(self._rx, self._reg(session)), "wsg_rx_clear")
+
+    def forget(self, session):
+        _check(self._L.wsg_rx_forget(self._rx, self._reg(session)), "wsg_rx_forget")
+
+    def pending(self):
+        f, b = ctypes.c_uint32(), ctypes.c_uint64()
+        _check(self._L.wsg_rx_pending(self._rx, ctypes.byref(f), ctypes.byref(b)), "wsg_rx_pending")
+        return f.value, b.value
+
+    def flush(self):
+        n = ctypes.c_uint32()
+        _check(self._L.wsg_rx_flush(self._rx, self._cb, None, ctypes.byref(n)), "wsg_rx_flush")
+        return n.value
+
+    def events(self, clear=True):
+        ev = list(self._events)
+        if clear:
+            self._events.clear()
+        return ev
 
 
 def info_to_numpy(info_tensor, n):

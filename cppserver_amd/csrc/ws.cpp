@@ -7,6 +7,7 @@
 // the gfx950 kernel behind wsg_xor_host.  Reference semantics followed:
 // source/server/ws/ws.cpp:212-498, including the quirks of SURVEY.md §8a.
 #include "server/ws/ws.h"
+#include "ws_session_impl.h"
 
 #include <cstdlib>
 #include <cstring>
@@ -124,11 +125,9 @@ bool WebSocket::PullHeaderField(const uint8_t*& data, size_t& size, size_t want,
     return true;
 }
 
-void WebSocket::DispatchMessage()
+void WebSocket::DispatchMessage(uint8_t opcode, const uint8_t* msg, size_t len)
 {
-    const uint8_t* msg = _ws_receive_final_buffer.data();
-    const size_t len = _ws_receive_final_buffer.size();
-    switch (_ws_opcode) {
+    switch (opcode) {
     case WS_PING:
         onWSPing(msg, len);
         break;
@@ -211,9 +210,27 @@ void WebSocket::PrepareReceiveFrame(const void* buffer, size_t size)
         _ws_frame_received = true;
         if (fin) {
             _ws_final_received = true;
-            DispatchMessage();
+            DispatchMessage(_ws_opcode, _ws_receive_final_buffer.data(), _ws_receive_final_buffer.size());
         }
     } while (size > 0);
+}
+
+void WebSocket::DeliverFrame(uint8_t opcode, bool fin, const uint8_t* payload, size_t len)
+{
+    if (_ws_final_received)
+        ResetMessage();
+    if (fin && _ws_receive_final_buffer.empty()) {
+        // a whole message in one frame: hand out the decoded payload where it
+        // lies (the reference hands out a pointer into its message buffer)
+        _ws_final_received = true;
+        DispatchMessage(opcode, payload, len);
+        return;
+    }
+    _ws_receive_final_buffer.insert(_ws_receive_final_buffer.end(), payload, payload + len);
+    if (fin) {
+        _ws_final_received = true;
+        DispatchMessage(opcode, _ws_receive_final_buffer.data(), _ws_receive_final_buffer.size());
+    }
 }
 
 size_t WebSocket::RequiredReceiveFrameSize()
@@ -250,24 +267,7 @@ void WebSocket::ClearWSBuffers()
 // C-ABI sessions (include/wsg_capi.h)
 // ===========================================================================
 
-struct wsg_session : public CppServer::WS::WebSocket {
-    explicit wsg_session(wsg_ctx* c) : WebSocket(c) {}
-    wsg_receive_cb cb = nullptr;
-    void* user = nullptr;
-
-    void emit(int kind, const void* b, size_t n, int status)
-    {
-        if (cb)
-            cb(user, kind, static_cast<const uint8_t*>(b), n, status);
-    }
-    void onWSReceived(const void* b, size_t n) override { emit(WSG_CB_RECEIVED, b, n, 0); }
-    void onWSClose(const void* b, size_t n, int status) override { emit(WSG_CB_CLOSE, b, n, status); }
-    void onWSPing(const void* b, size_t n) override { emit(WSG_CB_PING, b, n, 0); }
-    void onWSPong(const void* b, size_t n) override { emit(WSG_CB_PONG, b, n, 0); }
-
-    std::mutex& send_lock() { return _ws_send_lock; }
-    const std::vector<uint8_t>& send_buffer() const { return _ws_send_buffer; }
-};
+thread_local wsg_rx_dispatch g_rx_dispatch;
 
 extern "C" {
 

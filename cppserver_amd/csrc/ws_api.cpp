@@ -46,11 +46,26 @@ bool receive_message(std::vector<uint8_t>& out, Required required, Prepare prepa
 
 // ---------------------------------------------------------------- WSClient
 
+void WSClient::ResetBuffers()
+{
+    if (_rx_batch)
+        _rx_batch->Clear(*this);   // message state resets in delivery order
+    else
+        ClearWSBuffers();
+}
+
+void WSClient::SetReceiveBatch(WSReceiveBatch* batch)
+{
+    if (_rx_batch && _rx_batch != batch)
+        _rx_batch->Forget(*this);
+    _rx_batch = batch;
+}
+
 bool WSClient::Connect()
 {
     if (!_transport.IsConnected())
         return false;
-    ClearWSBuffers();
+    ResetBuffers();
     InitWSNonce();
     Handshaked(true);
     onWSConnected();
@@ -70,13 +85,17 @@ void WSClient::onDisconnected()
         _ws_handshaked = false;
         onWSDisconnected();
     }
-    ClearWSBuffers();
+    ResetBuffers();
     InitWSNonce();
 }
 
 void WSClient::onReceived(const void* buffer, size_t size)
 {
-    if (_ws_handshaked)
+    if (!_ws_handshaked)
+        return;
+    if (_rx_batch)
+        _rx_batch->Feed(*this, buffer, size);
+    else
         PrepareReceiveFrame(buffer, size);
 }
 
@@ -122,11 +141,26 @@ std::vector<uint8_t> WSClient::ReceiveBinary()
 
 // ---------------------------------------------------------------- WSSession
 
+void WSSession::ResetBuffers()
+{
+    if (_rx_batch)
+        _rx_batch->Clear(*this);   // message state resets in delivery order
+    else
+        ClearWSBuffers();
+}
+
+void WSSession::SetReceiveBatch(WSReceiveBatch* batch)
+{
+    if (_rx_batch && _rx_batch != batch)
+        _rx_batch->Forget(*this);
+    _rx_batch = batch;
+}
+
 bool WSSession::Connect()
 {
     if (!_transport.IsConnected())
         return false;
-    ClearWSBuffers();
+    ResetBuffers();
     Handshaked(false);
     onWSConnected();
     return true;
@@ -145,13 +179,17 @@ void WSSession::onDisconnected()
         _ws_handshaked = false;
         onWSDisconnected();
     }
-    ClearWSBuffers();
+    ResetBuffers();
     InitWSNonce();
 }
 
 void WSSession::onReceived(const void* buffer, size_t size)
 {
-    if (_ws_handshaked)
+    if (!_ws_handshaked)
+        return;
+    if (_rx_batch)
+        _rx_batch->Feed(*this, buffer, size);
+    else
         PrepareReceiveFrame(buffer, size);
 }
 
@@ -201,12 +239,38 @@ void WSServer::AddSession(const std::shared_ptr<WSSession>& session)
 {
     std::unique_lock<std::shared_mutex> locker(_sessions_lock);
     _sessions.push_back(session);
+    if (_rx_batch)
+        session->SetReceiveBatch(_rx_batch.get());
 }
 
 void WSServer::RemoveSession(const std::shared_ptr<WSSession>& session)
 {
     std::unique_lock<std::shared_mutex> locker(_sessions_lock);
+    if (_rx_batch && std::find(_sessions.begin(), _sessions.end(), session) != _sessions.end())
+        session->SetReceiveBatch(nullptr);   // its queued frames are dropped with it
     _sessions.erase(std::remove(_sessions.begin(), _sessions.end(), session), _sessions.end());
+}
+
+void WSServer::EnableBatchReceive(bool on)
+{
+    std::unique_lock<std::shared_mutex> locker(_sessions_lock);
+    if (on == (_rx_batch != nullptr))
+        return;
+    if (on) {
+        _rx_batch = std::make_unique<WSReceiveBatch>(codec());
+        for (auto& s : _sessions)
+            s->SetReceiveBatch(_rx_batch.get());
+        return;
+    }
+    for (auto& s : _sessions)
+        s->SetReceiveBatch(nullptr);
+    _rx_batch.reset();
+}
+
+size_t WSServer::FlushReceived()
+{
+    // not under _sessions_lock: callbacks may add or remove sessions
+    return _rx_batch ? _rx_batch->Flush() : 0;
 }
 
 size_t WSServer::sessions() const

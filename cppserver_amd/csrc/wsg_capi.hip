@@ -420,8 +420,10 @@ int wsg_fanout_encode(wsg_ctx* c, const uint8_t* d_payload, uint64_t len, const 
     hipStream_t s = pick(c, stream);
     const int t = timing_begin(c, s);
     const uint64_t pieces = uint64_t(k) * ((fsize + 15 + wsg::PIECE - 1) / wsg::PIECE);
-    WSG_HIP(wsg::launch_fanout(s, grid_for(c, ceil_div(pieces, wsg::BLOCK / 64)), d_payload, len, d_keys, k, opcode,
-                               mask ? 1u : 0u, fsize, d_wire));
+    const uint64_t blocks = wsg::fanout_flat ? ceil_div(ceil_div(total, wsg::CHUNK), wsg::BLOCK * wsg::FAN_UNITS)
+                                             : ceil_div(pieces, wsg::BLOCK / 64);
+    WSG_HIP(wsg::launch_fanout(s, grid_for(c, blocks), d_payload, len, d_keys, k, opcode, mask ? 1u : 0u, fsize,
+                               d_wire));
     timing_end(c, s, t);
     return WSG_OK;
 }

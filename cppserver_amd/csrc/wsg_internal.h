@@ -15,6 +15,11 @@ constexpr int UNROLL = WSG_UNROLL;          // steps per lane per tile
 constexpr uint64_t TILE = uint64_t(BLOCK) * CHUNK * UNROLL;   // 16 KiB of output
 constexpr int EU = 4;                                   // encode: 16-B steps per lane per piece
 constexpr uint64_t PIECE = uint64_t(64) * CHUNK * EU;   // encode work piece: 4 KiB of one frame
+#ifndef WSG_FANOUT_FLAT
+#define WSG_FANOUT_FLAT 1
+#endif
+constexpr bool fanout_flat = WSG_FANOUT_FLAT != 0;       // fan-out: flat chunk stream (else per-frame pieces)
+constexpr int FAN_UNITS = 4;                             // fan-out: 16-B chunks per lane per pass
 constexpr int SCAN_PER_LANE = 4;
 constexpr uint64_t SCAN_ITEMS = uint64_t(BLOCK) * SCAN_PER_LANE;   // frames per scan block
 

@@ -620,7 +620,7 @@ __device__ __forceinline__ void edge_chunk(const FrameRec& R, uint64_t p, uint8_
         }
         put_byte(w, j, b);
     }
-    if (own == 0xFFFFu) {
+    if (own == 0xFFFFu || (WSG_DIAG_ENC & 4)) {   // DIAG 4: full stores for shared chunks (timing only)
         st16nt(wire + p, w);
     } else {
 #pragma unroll
@@ -859,6 +859,92 @@ __global__ __launch_bounds__(BLOCK) void k_fanout(const uint8_t* __restrict__ pa
     }
 }
 
+// Flat variant: the k frames are one byte stream of k * fsize bytes, cut into
+// 16-byte chunks; every lane builds whole chunks (both frames' bytes where a
+// frame boundary falls inside one), so every store is a full 16-B store and
+// no cache line is written in parts by two waves.  The frame of a chunk is
+// p / fsize (a double-precision reciprocal, corrected by one).
+constexpr int FU = FAN_UNITS;
+
+__device__ __forceinline__ uint32_t fan_byte(const uint8_t* __restrict__ payload, const uint32_t* __restrict__ keys,
+                                             uint8_t opcode, bool mask, const SendGeom& g, uint64_t fsize, uint64_t i,
+                                             uint64_t r)
+{
+    const uint32_t key = keys[i];
+    if (r < g.hdr)
+        return header_byte(opcode, mask, g.body, key, uint32_t(r));
+    const uint64_t k = r - g.hdr;
+    if (k < g.prefix)
+        return key_byte(key, k);   // status 0: both prefix bytes are 0
+    return uint32_t(payload[k - g.prefix]) ^ key_byte(key, k);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_fanout_flat(const uint8_t* __restrict__ payload, uint64_t len,
+                                                       const uint32_t* __restrict__ keys, uint32_t k, uint8_t opcode,
+                                                       uint32_t mask, uint64_t fsize, double inv,
+                                                       uint8_t* __restrict__ wire)
+{
+    const SendGeom g = send_geom(opcode, mask != 0, len, 0);
+    const uint64_t total = fsize * k;
+    const uint64_t chunks = (total + CHUNK - 1) / CHUNK;
+    const uint64_t data0 = g.hdr + g.prefix;   // frame offset of the first payload byte
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t step = uint64_t(gridDim.x) * (BLOCK / 64) * (64 * FU);
+    for (uint64_t base = (uint64_t(blockIdx.x) * (BLOCK / 64) + wave_id()) * (64 * FU); base < chunks; base += step) {
+        v4u v[FU];
+#pragma unroll
+        for (int u = 0; u < FU; ++u) {
+            const uint64_t c = base + uint64_t(u) * 64 + lane;
+            v[u] = v4u{0, 0, 0, 0};
+            if (c >= chunks)
+                continue;
+            const uint64_t p = c * CHUNK;
+            uint64_t i = uint64_t(double(p) * inv);
+            int64_t r = int64_t(p - i * fsize);
+            if (r < 0) {
+                --i;
+                r += int64_t(fsize);
+            } else if (uint64_t(r) >= fsize) {
+                ++i;
+                r -= int64_t(fsize);
+            }
+            if (uint64_t(r) >= data0 && uint64_t(r) + CHUNK <= fsize) {
+                // all payload bytes of frame i
+                const uint64_t o = uint64_t(r) - data0;
+                const uintptr_t a = reinterpret_cast<uintptr_t>(payload) + o;
+                const uint32_t s = uint32_t(a & 15u);
+                const uint8_t* a0 = reinterpret_cast<const uint8_t*>(a - s);
+                const v4u lo = ld16(a0);
+                const v4u d = s ? funnel(lo, ld16(a0 + CHUNK), s) : lo;
+                v[u] = d ^ key_rot(keys[i], uint32_t(uint64_t(r) - g.hdr));
+            } else {
+                // header / status bytes, or a frame boundary inside the chunk
+                uint64_t ii = i, rr = uint64_t(r);
+#pragma unroll
+                for (uint32_t j = 0; j < CHUNK; ++j) {
+                    while (rr >= fsize) {
+                        rr -= fsize;
+                        ++ii;
+                    }
+                    if (ii < k)
+                        put_byte(v[u], j, fan_byte(payload, keys, opcode, mask != 0, g, fsize, ii, rr));
+                    ++rr;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < FU; ++u) {
+            const uint64_t c = base + uint64_t(u) * 64 + lane;
+            if (c + 1 < chunks || (c + 1 == chunks && (total & (CHUNK - 1)) == 0)) {
+                st16nt(wire + c * CHUNK, v[u]);
+            } else if (c + 1 == chunks) {
+                for (uint32_t j = 0; j < (total & (CHUNK - 1)); ++j)
+                    wire[c * CHUNK + j] = uint8_t(lane_byte(v[u], j));
+            }
+        }
+    }
+}
+
 // Single-buffer XOR used by the per-frame host path: dst[i] = src[i] ^
 // key[(phase + i) % 4].  src/dst 16-byte aligned device staging buffers.
 __global__ __launch_bounds__(BLOCK) void k_xor(const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,
@@ -922,7 +1008,10 @@ hipError_t launch_encode_mask(hipStream_t s, int grid, const uint8_t* payload, c
 hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64_t len, const uint32_t* keys,
                          uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire)
 {
-    k_fanout<<<grid, BLOCK, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, wire);
+    if (fanout_flat)
+        k_fanout_flat<<<grid, BLOCK, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, 1.0 / double(fsize), wire);
+    else
+        k_fanout<<<grid, BLOCK, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, wire);
     return hipGetLastError();
 }
 

@@ -29,6 +29,8 @@
 namespace CppServer {
 namespace WS {
 
+class WSReceiveBatch;
+
 //! GPU codec context of the calling thread (one wsg_ctx per host thread,
 //! device from $WSG_DEVICE, default 0).  Throws std::runtime_error when no
 //! device is available: there is no CPU fallback.
@@ -78,6 +80,9 @@ public:
     void set_send_key(uint32_t key) noexcept;
 
 protected:
+    //! Codec context of this connection (the explicit one, else ThreadCodec())
+    wsg_ctx* codec();
+
     virtual void onWSConnected() {}
     virtual void onWSDisconnected() {}
     virtual void onWSReceived(const void* buffer, size_t size) {}
@@ -113,14 +118,18 @@ protected:
     std::array<uint8_t, 16> _ws_nonce{};
 
 private:
+    friend class WSReceiveBatch;   // batched receive: framing here, unmask in one launch per flush
+
     wsg_ctx* _codec{nullptr};
-    wsg_ctx* codec();
     // append `want` bytes of the input to the frame buffer (full field width,
     // the reference's split-header behaviour)
     bool PullHeaderField(const uint8_t*& data, size_t& size, size_t want, uint8_t* mirror = nullptr);
     void ResetFrame();
     void ResetMessage();
-    void DispatchMessage();
+    void DispatchMessage(uint8_t opcode, const uint8_t* msg, size_t len);
+    // message half of PrepareReceiveFrame for one decoded frame (batched
+    // receive): append to the message, dispatch on FIN (ws.cpp:399-452)
+    void DeliverFrame(uint8_t opcode, bool fin, const uint8_t* payload, size_t len);
 };
 
 } // namespace WS

@@ -11,6 +11,7 @@
 #define CPPSERVER_AMD_WS_CLIENT_H
 
 #include "server/ws/ws.h"
+#include "server/ws/ws_batch.h"
 #include "server/ws/ws_transport.h"
 
 namespace CppServer {
@@ -67,6 +68,8 @@ public:
 
     //! Bytes read by the transport (the reference's TCPClient::onReceived override)
     void onReceived(const void* buffer, size_t size);
+    //! Route this client's receive path through `batch` (nullptr: per call, ws_batch.h)
+    void SetReceiveBatch(WSReceiveBatch* batch);
     //! Transport closed (reference ws_client.cpp:56-74)
     void onDisconnected();
 
@@ -80,6 +83,8 @@ protected:
     Transport& _transport;
 
 private:
+    WSReceiveBatch* _rx_batch{nullptr};
+    void ResetBuffers();
     size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0);
     bool SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status = 0);
     bool ReceiveMessage(std::vector<uint8_t>& out);

@@ -22,7 +22,7 @@ class WSServer : protected WebSocket
 {
 public:
     explicit WSServer(wsg_ctx* codec = nullptr) : WebSocket(codec) {}
-    virtual ~WSServer() = default;
+    virtual ~WSServer() { EnableBatchReceive(false); }
 
     //! Register / unregister a connected session (the reference's TCPServer session map)
     void AddSession(const std::shared_ptr<WSSession>& session);
@@ -44,8 +44,19 @@ public:
     size_t MulticastPing(const void* buffer, size_t size) { return MulticastFrame(WS_FIN | WS_PING, buffer, size); }
     size_t MulticastPing(std::string_view text) { return MulticastFrame(WS_FIN | WS_PING, text.data(), text.size()); }
 
+    //! Batched receive: every registered session's
+    //! bytes are framed into one WSReceiveBatch and unmasked in one GPU pass
+    //! per FlushReceived(), which fires the sessions' onWS* in arrival order.
+    void EnableBatchReceive(bool on);
+    bool IsBatchReceive() const { return _rx_batch != nullptr; }
+    //! Decode and deliver everything the sessions received since the last
+    //! flush; returns the number of frames delivered
+    size_t FlushReceived();
+
 private:
     size_t MulticastFrame(uint8_t opcode, const void* buffer, size_t size);
+
+    std::unique_ptr<WSReceiveBatch> _rx_batch;
 
     mutable std::shared_mutex _sessions_lock;
     std::vector<std::shared_ptr<WSSession>> _sessions;

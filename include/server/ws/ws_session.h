@@ -8,6 +8,7 @@
 #define CPPSERVER_AMD_WS_SESSION_H
 
 #include "server/ws/ws.h"
+#include "server/ws/ws_batch.h"
 #include "server/ws/ws_transport.h"
 
 namespace CppServer {
@@ -61,8 +62,12 @@ public:
     std::string ReceiveText();
     std::vector<uint8_t> ReceiveBinary();
 
-    //! Bytes read by the transport (reference ws_session.cpp:40-51)
+    //! Bytes read by the transport (reference ws_session.cpp:40-51).  With a
+    //! receive batch set they are framed into the batch, and the onWS*
+    //! callbacks fire at the batch's next Flush() (ws_batch.h).
     void onReceived(const void* buffer, size_t size);
+    //! Route this session's receive path through `batch` (nullptr: per call)
+    void SetReceiveBatch(WSReceiveBatch* batch);
     //! Transport closed (reference ws_session.cpp:20-38)
     void onDisconnected();
 
@@ -73,6 +78,8 @@ protected:
     Transport& _transport;
 
 private:
+    WSReceiveBatch* _rx_batch{nullptr};
+    void ResetBuffers();
     size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0);
     bool SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status = 0);
     bool ReceiveMessage(std::vector<uint8_t>& out);

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define WSG_ABI_VERSION 1
+#define WSG_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 #define WSG_OK          0
@@ -178,6 +178,29 @@ int wsg_session_prepare_receive(wsg_session* s, const void* buf, size_t size,
 size_t wsg_session_required(wsg_session* s);
 /* ClearWSBuffers (ws.cpp:484).                                                */
 int wsg_session_clear(wsg_session* s);
+
+/* ---- batched receive over many sessions ---------- */
+/* The host framer + session batcher: wsg_rx_feed runs a session's framing
+ * state machine (PrepareReceiveFrame's header half, ws.cpp:292-397, the
+ * split-header behaviour of SURVEY Q7 included) and appends each completed
+ * frame to one page-locked batch; wsg_rx_flush unmasks the batch in one GPU
+ * pass (wsg_decode_batch_host) and delivers the frames in arrival order
+ * through each session's message logic (ws.cpp:399-452).  Every session sees
+ * the callbacks wsg_session_prepare_receive would have fired, in the same
+ * order.  Callback data stays valid until the next flush.  One thread.      */
+typedef struct wsg_rx wsg_rx;
+typedef void (*wsg_rx_cb)(void* user, wsg_session* s, int kind,
+                          const uint8_t* data, size_t size, int status);
+int wsg_rx_create(wsg_ctx* ctx, wsg_rx** out);
+int wsg_rx_destroy(wsg_rx* rx);
+int wsg_rx_feed(wsg_rx* rx, wsg_session* s, const void* buf, size_t size);
+/* ClearWSBuffers (ws.cpp:484) for a batched session, in delivery order.       */
+int wsg_rx_clear(wsg_rx* rx, wsg_session* s);
+/* Drop a session's queued frames (before wsg_session_destroy).                */
+int wsg_rx_forget(wsg_rx* rx, wsg_session* s);
+/* Complete frames and wire bytes queued for the next flush.                   */
+int wsg_rx_pending(wsg_rx* rx, uint32_t* frames, uint64_t* bytes);
+int wsg_rx_flush(wsg_rx* rx, wsg_rx_cb cb, void* user, uint32_t* delivered);
 
 /* ---- kernel timing (measurement hook used by bench.py) ------------------ */
 /* on = k > 0: the ctx records HIP events around the dominant payload kernel of

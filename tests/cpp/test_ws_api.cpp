@@ -247,6 +247,84 @@ static void test_soak()
     CHECK(sent_total == echoed_total);
 }
 
+// Server-side batched receive: sessions' bytes are
+// framed into one batch and unmasked in one GPU pass per FlushReceived();
+// callbacks (and so the echoes) happen only at the flush, in arrival order.
+static void test_batched_server_receive()
+{
+    WSServer server;
+    std::vector<std::unique_ptr<Pair>> pairs;
+    for (int i = 0; i < 8; ++i) {
+        pairs.emplace_back(new Pair());
+        server.AddSession(pairs.back()->session);
+    }
+    server.EnableBatchReceive(true);
+    CHECK(server.IsBatchReceive());
+    std::mt19937 gen(99);
+    std::vector<std::vector<std::vector<uint8_t>>> sent(pairs.size());
+    // hand a session its inbox in random-sized reads, as TryReceive would
+    auto deliver = [&](Pair& p) {
+        std::vector<uint8_t> b(p.st.inbox.begin(), p.st.inbox.end());
+        p.st.inbox.clear();
+        for (size_t at = 0; at < b.size();) {
+            const size_t n = std::min<size_t>(b.size() - at, 1 + gen() % 5000);
+            p.session->onReceived(b.data() + at, n);
+            at += n;
+        }
+    };
+    for (int round = 0; round < 6; ++round) {
+        size_t frames = 0;
+        for (size_t i = 0; i < pairs.size(); ++i) {
+            const int k = 1 + int(gen() % 3);
+            for (int j = 0; j < k; ++j) {
+                std::vector<uint8_t> payload((gen() % 4 == 0) ? gen() % 70000 : gen() % 300);
+                for (auto& b : payload)
+                    b = uint8_t(gen());
+                pairs[i]->client->SendBinaryAsync(payload.data(), payload.size());
+                sent[i].push_back(payload);
+                ++frames;
+            }
+        }
+        for (auto& p : pairs)
+            deliver(*p);
+        bool quiet = true;
+        for (auto& p : pairs)
+            quiet = quiet && p->ct.inbox.empty() && p->session->last.empty();
+        CHECK(quiet);   // nothing delivered before the flush
+        CHECK(server.FlushReceived() == frames);
+        for (auto& p : pairs) {
+            p->session->last.clear();
+            p->pump();   // echoes back to the (per-call) clients
+        }
+    }
+    for (size_t i = 0; i < pairs.size(); ++i)
+        CHECK(pairs[i]->client->messages == sent[i]);
+
+    // control frames through the batch: ping -> pong, close with status
+    pairs[0]->client->SendPingAsync("ab");
+    deliver(*pairs[0]);
+    CHECK(pairs[0]->client->pongs.empty());
+    CHECK(server.FlushReceived() == 1);
+    pairs[0]->pump();
+    CHECK(pairs[0]->client->pongs.size() == 1 &&
+          pairs[0]->client->pongs[0] == std::vector<uint8_t>({0, 0, 0, 0, 'a', 'b'}));
+    pairs[1]->client->SendCloseAsync(1001, "bye");
+    deliver(*pairs[1]);
+    CHECK(server.FlushReceived() == 1);
+    CHECK(pairs[1]->session->closes == 1 && pairs[1]->session->close_status == 1001);
+
+    // a removed session's queued frames are dropped, the others still arrive
+    pairs[2]->client->SendTextAsync("gone");
+    pairs[3]->client->SendTextAsync("kept");
+    deliver(*pairs[2]);
+    deliver(*pairs[3]);
+    server.RemoveSession(pairs[2]->session);
+    CHECK(server.FlushReceived() == 1);
+    CHECK(std::string(pairs[3]->session->last.begin(), pairs[3]->session->last.end()) == "kept");
+    server.EnableBatchReceive(false);
+    CHECK(!server.IsBatchReceive());
+}
+
 int main()
 {
     try {
@@ -255,6 +333,7 @@ int main()
         test_ping_pong_and_close();
         test_sync_receive();
         test_soak();
+        test_batched_server_receive();
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());
         return 2;

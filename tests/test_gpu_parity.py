@@ -220,6 +220,26 @@ def test_fanout_shapes(codec, length, k, opcode, mask):
     assert np.array_equal(wire.cpu().numpy()[: len(ref)], ref)
 
 
+@pytest.mark.parametrize("length,k,opcode,mask,src_off", [(2, 50, 0x82, True, 0), (3, 41, 0x89, True, 1),
+                                                         (7, 64, 0x82, False, 5), (9, 17, 0x88, True, 0),
+                                                         (10, 300, 0x81, True, 3), (4096, 257, 0x82, True, 7),
+                                                         (65535, 5, 0x82, True, 9)])
+def test_fanout_tiny_unaligned_tail(codec, length, k, opcode, mask, src_off):
+    """Frames shorter than a 16-B chunk, payloads at any alignment, and no byte
+    written past the k frames (sentinel-filled wire)."""
+    payload, keys = wl.c4_fanout(length, k, seed=7 * length + k)
+    ref = oracle.fanout_encode(payload, keys, opcode, mask)
+    buf = np.zeros(length + src_off + 1, np.uint8)
+    buf[src_off: src_off + length] = payload
+    pbuf = dev(buf)
+    wire = torch.full((len(ref) + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    codec.fanout(pbuf[src_off:], dev(keys.view(np.int32)), opcode, mask, wire=wire, length=length)
+    codec.sync()
+    got = wire.cpu().numpy()
+    assert np.array_equal(got[: len(ref)], ref)
+    assert (got[len(ref):] == 0xA5).all()
+
+
 # ---------------------------------------------------------------- edge cases
 def test_empty_batches(codec):
     rc, out, info = gpu_decode(codec, np.zeros(32, np.uint8), [])

@@ -13,5 +13,6 @@ $H $F -c $root/cppserver_amd/csrc/wsg_kernels.hip -o k.o
 $H $F -c $root/cppserver_amd/csrc/wsg_capi.hip -o c.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws.cpp -o w.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws_api.cpp -o a.o
-$H --offload-arch=gfx950 -shared -o libwsg.so k.o c.o w.o a.o
+$H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws_batch.cpp -o b.o
+$H --offload-arch=gfx950 -shared -o libwsg.so k.o c.o w.o a.o b.o
 echo "$out/libwsg.so"

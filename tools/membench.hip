@@ -71,6 +71,53 @@ __global__ __launch_bounds__(BLOCK) void k_wavepiece(const u32x4* __restrict__ s
     }
 }
 
+// Write-only stream (the fan-out's shape): every lane stores U chunks.
+template <int BLOCK, int U, int NT>
+__global__ __launch_bounds__(BLOCK) void k_fill(u32x4* __restrict__ dst, uint64_t n16, uint32_t key)
+{
+    const uint64_t per_tile = uint64_t(BLOCK) * U;
+    for (uint64_t t = blockIdx.x; t * per_tile < n16; t += gridDim.x) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = t * per_tile + uint64_t(u) * BLOCK + threadIdx.x;
+            if (i < n16) {
+                const u32x4 w = u32x4{uint32_t(i), key, key, key};
+                if (NT)
+                    __builtin_nontemporal_store(w, dst + i);
+                else
+                    dst[i] = w;
+            }
+        }
+    }
+}
+
+template <int BLOCK, int U, int NT>
+void run_fill(u32x4* dst, uint64_t n16, int grid, bool single)
+{
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i)
+        k_fill<BLOCK, U, NT><<<grid, BLOCK>>>(dst, n16, 7u);
+    const int reps = single ? 1 : 20;
+    float tot = 0;
+    for (int r = 0; r < (single ? 20 : 1); ++r) {
+        CK(hipEventRecord(a));
+        for (int i = 0; i < reps; ++i)
+            k_fill<BLOCK, U, NT><<<grid, BLOCK>>>(dst, n16, 7u);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        tot += ms;
+    }
+    const double ms = tot / 20;
+    printf("fill %s U=%2d nt=%d grid=%6d  %8.2f us  %7.1f GB/s\n", single ? "single " : "b2b    ", U, NT, grid,
+           ms * 1e3, n16 * 16 / (ms * 1e-3) / 1e9);
+    CK(hipEventDestroy(a));
+    CK(hipEventDestroy(b));
+}
+
 template <int BLOCK, int U>
 void run_wp(const char* name, const u32x4* src, u32x4* dst, uint64_t n16, int cus, int bpc)
 {
@@ -123,7 +170,7 @@ void run(const char* name, const u32x4* src, u32x4* dst, uint64_t n16, int cus, 
 int main(int argc, char** argv)
 {
     const uint64_t mib = argc > 1 ? strtoull(argv[1], 0, 10) : 256;
-    const uint64_t bytes = mib << 20;
+    const uint64_t bytes = (mib ? mib : 64) << 20;   // 0 = write mode's fan-out size, in a 64 MiB buffer
     const uint64_t n16 = bytes / 16;
     hipDeviceProp_t p;
     CK(hipGetDeviceProperties(&p, 0));
@@ -141,6 +188,36 @@ int main(int argc, char** argv)
             run_wp<256, 4>("wave-piece 4K", src, dst, n16, cus, 32);
             run_wp<256, 8>("wave-piece 8K", src, dst, n16, cus, 16);
             run_wp<256, 16>("wave-piece 16K", src, dst, n16, cus, 8);
+        }
+        CK(hipFree(src));
+        CK(hipFree(dst));
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "write") {
+        // write-only floor for a fan-out-sized output (argv[1] MiB; 0 = 41,040,000 B)
+        const uint64_t w16 = mib ? n16 : 41040000ull / 16;
+        if (w16 > n16) {
+            fprintf(stderr, "write size exceeds the buffer\n");
+            return 1;
+        }
+        for (int single = 0; single < 2; ++single) {
+            for (int grid : {cus * 4, cus * 8, cus * 16, int((w16 + 1023) / 1024)}) {
+                run_fill<256, 4, 1>(dst, w16, grid, single);
+                run_fill<256, 4, 0>(dst, w16, grid, single);
+            }
+            run_fill<256, 16, 1>(dst, w16, int((w16 + 4095) / 4096), single);
+            run_fill<256, 1, 1>(dst, w16, int((w16 + 255) / 256), single);
+            hipEvent_t a, b;
+            CK(hipEventCreate(&a));
+            CK(hipEventCreate(&b));
+            CK(hipEventRecord(a));
+            for (int i = 0; i < 20; ++i)
+                CK(hipMemsetAsync(dst, i, w16 * 16));
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, a, b));
+            printf("hipMemsetAsync b2b  %8.2f us\n", ms / 20 * 1e3);
         }
         CK(hipFree(src));
         CK(hipFree(dst));

@@ -17,6 +17,8 @@ from cppserver_amd import workloads as wl  # noqa: E402
 def main():
     libs = sys.argv[1:] or [None]
     cfg = os.environ.get("CFG", "c5")
+    if cfg == "c4":
+        return fanout(libs)
     if cfg == "c5":
         payload, desc, _ = wl.c5_shard(0, 8, n_total=1 << 20)      # one rank's share of 8: 131072 x 16 KiB
     else:
@@ -46,6 +48,32 @@ def main():
     for l, k in zip(libs, kern):
         m = statistics.median(k)
         print("%-50s encode kernel %.4f ms  %.0f GB/s  spread %.1f%%" % (l, m, alg / m / 1e6,
+                                                                       100 * (max(k) - min(k)) / m))
+
+
+def fanout(libs):
+    payload, keys = wl.c4_fanout(int(os.environ.get("LEN", 4096)), int(os.environ.get("KEYS", 10000)))
+    fsz = ca.frame_size(0x82, True, len(payload))
+    p = torch.from_numpy(payload).cuda()
+    kt = torch.from_numpy(keys.view(np.int32)).cuda()
+    wires = [torch.empty(fsz * len(keys), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    codecs = [ca.Codec(0, lib_path=l) for l in libs]
+    kern = [[] for _ in libs]
+    for rep in range(int(os.environ.get("REPS", 5))):
+        for ci, c in enumerate(codecs):
+            for it in range(3):
+                c.fanout(p, kt, 0x82, True, wire=wires[it & 1])
+            c.timing(True, 1)
+            c.timing_read()
+            for it in range(20):
+                c.fanout(p, kt, 0x82, True, wire=wires[it & 1])
+            ms, k = c.timing_read()
+            c.timing(False)
+            kern[ci].append(ms / k)
+    alg = len(payload) + 4 * len(keys) + fsz * len(keys)
+    for l, k in zip(libs, kern):
+        m = statistics.median(k)
+        print("%-50s fanout kernel %.4f ms  %.0f GB/s  spread %.1f%%" % (l, m, alg / m / 1e6,
                                                                        100 * (max(k) - min(k)) / m))
 
 
