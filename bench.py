@@ -272,6 +272,32 @@ def pcie_inclusive(w, reps=3):
     return res
 
 
+def session_batch_leg(timeout=240):
+    """The batched session paths end to end on host
+    buffers: C2's 4096 x 64 KiB frames spread over 1024 sessions, framed on
+    the host (16 KiB reads), unmasked in one pipelined GPU pass, delivered
+    through each session's callbacks; and the same frames queued for send and
+    encoded in one pass.  Beside it, the per-call GPU path (one
+    PrepareReceiveFrame / PrepareSendFrame per frame).  Runs
+    tools/_build/bench_batch (product library only) as a child process."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "tools", "_build", "bench_batch")
+    if not os.path.exists(exe):
+        return None
+    out = {}
+    for mode, args in (("rx", ["1024", "4", "65536", "16384", "3"]), ("tx", ["1024", "4", "65536", "0", "3"])):
+        r = subprocess.run([exe, mode] + args, capture_output=True, text=True, timeout=timeout)
+        if r.returncode != 0:
+            out[mode] = {"error": (r.stderr or r.stdout).strip()[-300:]}
+            continue
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        out[mode] = {k: d[k] for k in ("batched_GiBps", "per_call_GiBps", "batched_frames_per_s",
+                                       "per_call_frames_per_s", "delivered_ok")}
+    out["workload"] = "1024 sessions x 4 frames x 64 KiB, host buffers (PCIe + host framing + callbacks inside)"
+    return out
+
+
 def gather_leg(w, world, device):
     """C5's exchange step: every rank's framed output to rank 0 over RCCL
     (variable-size grouped send/recv, cppserver_amd.shard.gather_frames),
@@ -343,6 +369,10 @@ def main():
         pc = pcie_inclusive(w)
         if pc is not None:
             extras["pcie_inclusive_GiBps"] = pc
+        if w.cfg == "c2":
+            sb = session_batch_leg()
+            if sb is not None:
+                extras["session_batch"] = sb
     cpu1 = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu1, cpu_mt = cpu_baseline(w, args.cpu_seconds)

@@ -62,6 +62,7 @@ def lib(path=None):
         "wsg_fanout_encode": (ci, [vp, vp, u64, vp, u32, ctypes.c_uint8, ci, vp, u64, vp]),
         "wsg_xor_host": (ci, [vp, vp, vp, sz, u32, u32]),
         "wsg_decode_batch_host": (ci, [vp, vp, u64, vp, u32, vp, vp]),
+        "wsg_encode_batch_host": (ci, [vp, vp, u64, vp, u32, vp, u64, vp]),
         "wsg_host_alloc": (ci, [sz, ctypes.POINTER(vp)]),
         "wsg_host_free": (ci, [vp]),
         "wsg_frame_size": (u64, [ctypes.c_uint8, ci, u64, i32]),
@@ -81,6 +82,12 @@ def lib(path=None):
         "wsg_rx_forget": (ci, [vp, vp]),
         "wsg_rx_pending": (ci, [vp, ctypes.POINTER(u32), ctypes.POINTER(u64)]),
         "wsg_rx_flush": (ci, [vp, vp, vp, ctypes.POINTER(u32)]),
+        "wsg_tx_create": (ci, [vp, ctypes.POINTER(vp)]),
+        "wsg_tx_destroy": (ci, [vp]),
+        "wsg_tx_queue": (ci, [vp, vp, ctypes.c_uint8, ci, vp, sz, i32]),
+        "wsg_tx_forget": (ci, [vp, vp]),
+        "wsg_tx_pending": (ci, [vp, ctypes.POINTER(u32), ctypes.POINTER(u64)]),
+        "wsg_tx_flush": (ci, [vp, vp, vp, ctypes.POINTER(u32)]),
         "wsg_timing_enable": (ci, [vp, ci]),
         "wsg_timing_read": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ci]),
     }
@@ -247,6 +254,19 @@ class Codec:
                                            _np_ptr(out), _np_ptr(info))
         return rc, out[: len(wire)], info[: len(fs)]
 
+    def encode_batch_host(self, payload, desc, wire=None):
+        """Host-staged batch encode: returns (rc, wire bytes, wire_off)."""
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc, dtype=SEND_DESC)
+        n = len(desc)
+        total = int(sum(frame_size(int(d["opcode"]), bool(d["mask"]), int(d["len"]), int(d["status"])) for d in desc))
+        if wire is None:
+            wire = np.empty(max(total, 1), dtype=np.uint8)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        rc = self._L.wsg_encode_batch_host(self._ctx, _np_ptr(payload) if len(payload) else None, len(payload),
+                                           _np_ptr(desc) if n else None, n, _np_ptr(wire), len(wire), _np_ptr(off))
+        return rc, wire[:total], off
+
     # -- measurement hooks ----------------------------------------------------
     def timing(self, on=True, every=1):
         """Time the dominant kernel of every `every`-th batch call (HIP events)."""
@@ -377,6 +397,58 @@ class RxBatch:
         if clear:
             self._events.clear()
         return ev
+
+
+TX_SINK = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t)
+
+
+class TxBatch:
+    """Batched send over many sessions through the C-ABI (wsg_tx_*): queue()
+    records a PrepareSendFrame call, flush() encodes all of them in one GPU
+    pass and returns [(session, frame bytes)] in queue order."""
+
+    def __init__(self, codec):
+        self._L = lib()
+        self._codec = codec
+        tx = ctypes.c_void_p()
+        _check(self._L.wsg_tx_create(codec._ctx, ctypes.byref(tx)), "wsg_tx_create")
+        self._tx = tx
+        self._out = []
+        self._by_ptr = {}
+
+        def _sink(user, sess, frame, size):
+            self._out.append((self._by_ptr.get(sess), ctypes.string_at(frame, size)))
+
+        self._sink = TX_SINK(_sink)
+
+    def close(self):
+        if getattr(self, "_tx", None):
+            self._L.wsg_tx_destroy(self._tx)
+            self._tx = None
+
+    __del__ = close
+
+    def queue(self, session, opcode, mask, payload=b"", status=0):
+        self._by_ptr[session._s.value] = session
+        buf = bytes(payload)
+        _check(self._L.wsg_tx_queue(self._tx, session._s, opcode, 1 if mask else 0, buf if buf else None, len(buf),
+                                    status), "wsg_tx_queue")
+
+    def forget(self, session):
+        _check(self._L.wsg_tx_forget(self._tx, session._s), "wsg_tx_forget")
+
+    def pending(self):
+        f, b = ctypes.c_uint32(), ctypes.c_uint64()
+        _check(self._L.wsg_tx_pending(self._tx, ctypes.byref(f), ctypes.byref(b)), "wsg_tx_pending")
+        return f.value, b.value
+
+    def flush(self):
+        n = ctypes.c_uint32()
+        self._out = []
+        _check(self._L.wsg_tx_flush(self._tx, self._sink, None, ctypes.byref(n)), "wsg_tx_flush")
+        out, self._out = self._out, []
+        assert len(out) == n.value
+        return out
 
 
 def info_to_numpy(info_tensor, n):

@@ -99,8 +99,18 @@ void WSClient::onReceived(const void* buffer, size_t size)
         PrepareReceiveFrame(buffer, size);
 }
 
+void WSClient::SetSendBatch(WSSendBatch* batch)
+{
+    std::scoped_lock locker(_ws_send_lock);
+    if (_tx_batch && _tx_batch != batch)
+        _tx_batch->Forget(_transport);
+    _tx_batch = batch;
+}
+
 size_t WSClient::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status)
 {
+    if (_tx_batch)
+        _tx_batch->Flush();   // earlier async frames go first
     std::scoped_lock locker(_ws_send_lock);
     PrepareSendFrame(opcode, true, buffer, size, status);
     return _transport.Send(_ws_send_buffer.data(), _ws_send_buffer.size());
@@ -109,6 +119,10 @@ size_t WSClient::SendFrame(uint8_t opcode, const void* buffer, size_t size, int 
 bool WSClient::SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status)
 {
     std::scoped_lock locker(_ws_send_lock);
+    if (_tx_batch) {
+        _tx_batch->Queue(_transport, send_key(), opcode, true, buffer, size, status);
+        return true;
+    }
     PrepareSendFrame(opcode, true, buffer, size, status);
     return _transport.SendAsync(_ws_send_buffer.data(), _ws_send_buffer.size());
 }
@@ -193,8 +207,18 @@ void WSSession::onReceived(const void* buffer, size_t size)
         PrepareReceiveFrame(buffer, size);
 }
 
+void WSSession::SetSendBatch(WSSendBatch* batch)
+{
+    std::scoped_lock locker(_ws_send_lock);
+    if (_tx_batch && _tx_batch != batch)
+        _tx_batch->Forget(_transport);
+    _tx_batch = batch;
+}
+
 size_t WSSession::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status)
 {
+    if (_tx_batch)
+        _tx_batch->Flush();   // earlier async frames go first
     std::scoped_lock locker(_ws_send_lock);
     PrepareSendFrame(opcode, false, buffer, size, status);
     return _transport.Send(_ws_send_buffer.data(), _ws_send_buffer.size());
@@ -203,6 +227,10 @@ size_t WSSession::SendFrame(uint8_t opcode, const void* buffer, size_t size, int
 bool WSSession::SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status)
 {
     std::scoped_lock locker(_ws_send_lock);
+    if (_tx_batch) {
+        _tx_batch->Queue(_transport, send_key(), opcode, false, buffer, size, status);
+        return true;
+    }
     PrepareSendFrame(opcode, false, buffer, size, status);
     return _transport.SendAsync(_ws_send_buffer.data(), _ws_send_buffer.size());
 }
@@ -241,13 +269,19 @@ void WSServer::AddSession(const std::shared_ptr<WSSession>& session)
     _sessions.push_back(session);
     if (_rx_batch)
         session->SetReceiveBatch(_rx_batch.get());
+    if (_tx_batch)
+        session->SetSendBatch(_tx_batch.get());
 }
 
 void WSServer::RemoveSession(const std::shared_ptr<WSSession>& session)
 {
     std::unique_lock<std::shared_mutex> locker(_sessions_lock);
-    if (_rx_batch && std::find(_sessions.begin(), _sessions.end(), session) != _sessions.end())
-        session->SetReceiveBatch(nullptr);   // its queued frames are dropped with it
+    if (std::find(_sessions.begin(), _sessions.end(), session) != _sessions.end()) {
+        if (_rx_batch)
+            session->SetReceiveBatch(nullptr);   // its queued frames are dropped with it
+        if (_tx_batch)
+            session->SetSendBatch(nullptr);
+    }
     _sessions.erase(std::remove(_sessions.begin(), _sessions.end(), session), _sessions.end());
 }
 
@@ -267,6 +301,26 @@ void WSServer::EnableBatchReceive(bool on)
     _rx_batch.reset();
 }
 
+void WSServer::EnableBatchSend(bool on)
+{
+    if (!on && _tx_batch)
+        _tx_batch->Flush();   // nothing queued is lost
+    std::unique_lock<std::shared_mutex> locker(_sessions_lock);
+    if (on == (_tx_batch != nullptr))
+        return;
+    if (on) {
+        _tx_batch = std::make_unique<WSSendBatch>(codec());
+        for (auto& s : _sessions)
+            s->SetSendBatch(_tx_batch.get());
+        return;
+    }
+    for (auto& s : _sessions)
+        s->SetSendBatch(nullptr);
+    _tx_batch.reset();
+}
+
+size_t WSServer::FlushSend() { return _tx_batch ? _tx_batch->Flush() : 0; }
+
 size_t WSServer::FlushReceived()
 {
     // not under _sessions_lock: callbacks may add or remove sessions
@@ -285,6 +339,8 @@ bool WSServer::Multicast(const void* buffer, size_t size)
         return true;
     if (buffer == nullptr)
         return false;
+    if (_tx_batch)
+        _tx_batch->Flush();   // queued frames precede the multicast on every session
     std::shared_lock<std::shared_mutex> locker(_sessions_lock);
     for (auto& session : _sessions) {
         std::scoped_lock ws_locker(session->_ws_send_lock);

@@ -1,5 +1,5 @@
-// ws_batch.cpp — batched receive for many connections (include/server/ws/ws_batch.h)
-// and its C-ABI (wsg_rx_*, include/wsg_capi.h).
+// ws_batch.cpp — batched receive and send for many connections
+// (include/server/ws/ws_batch.h) and their C-ABI (wsg_rx_*, wsg_tx_*).
 //
 // Feed() is the framing half of the reference's PrepareReceiveFrame
 // (source/server/ws/ws.cpp:292-397) run on the connection's own state; the
@@ -7,6 +7,7 @@
 // message half (ws.cpp:407-452) WebSocket::DeliverFrame, called in arrival
 // order.
 #include "server/ws/ws_batch.h"
+#include "server/ws/ws_transport.h"
 #include "ws_session_impl.h"
 
 #include <algorithm>
@@ -210,6 +211,125 @@ size_t WSReceiveBatch::Flush()
     return delivered;
 }
 
+// ---------------------------------------------------------------- send batch
+
+namespace {
+
+void grow_pinned(uint8_t*& p, uint64_t& cap, uint64_t len, uint64_t need)
+{
+    if (need <= cap)
+        return;
+    const uint64_t ncap = std::max<uint64_t>(need, std::max<uint64_t>(2 * cap, uint64_t(1) << 20));
+    void* q = nullptr;
+    check(wsg_host_alloc(ncap, &q), "wsg_host_alloc");
+    if (len)
+        std::memcpy(q, p, len);
+    if (p)
+        wsg_host_free(p);
+    p = static_cast<uint8_t*>(q);
+    cap = ncap;
+}
+
+} // namespace
+
+WSSendBatch::WSSendBatch(wsg_ctx* codec) : _ctx(codec) {}
+
+WSSendBatch::~WSSendBatch()
+{
+    if (_payload.p)
+        wsg_host_free(_payload.p);
+    if (_wire.p)
+        wsg_host_free(_wire.p);
+}
+
+void WSSendBatch::Push(Transport* t, void* tag, uint32_t key, uint8_t opcode, bool mask, const void* buffer,
+                       size_t size, int status)
+{
+    if (size && !buffer)
+        throw std::invalid_argument("WSSendBatch: null payload");
+    grow_pinned(_payload.p, _payload.cap, _payload.len, _payload.len + size);
+    wsg_send_desc d{};
+    d.src_off = _payload.len;
+    d.len = size;
+    d.key = key;
+    d.status = status;
+    d.opcode = opcode;
+    d.mask = mask ? 1 : 0;
+    if (size)
+        std::memcpy(_payload.p + _payload.len, buffer, size);
+    _payload.len += size;
+    _desc.push_back(d);
+    _recs.push_back(Rec{t, tag});
+}
+
+void WSSendBatch::Queue(Transport& transport, uint32_t key, uint8_t opcode, bool mask, const void* buffer,
+                        size_t size, int status)
+{
+    Push(&transport, nullptr, key, opcode, mask, buffer, size, status);
+}
+
+void WSSendBatch::Queue(void* tag, uint32_t key, uint8_t opcode, bool mask, const void* buffer, size_t size,
+                        int status)
+{
+    Push(nullptr, tag, key, opcode, mask, buffer, size, status);
+}
+
+void WSSendBatch::Forget(Transport& transport)
+{
+    for (Rec& r : _recs)
+        if (r.transport == &transport)
+            r = Rec{nullptr, nullptr};
+}
+
+void WSSendBatch::Forget(void* tag)
+{
+    for (Rec& r : _recs)
+        if (r.tag == tag && !r.transport)
+            r = Rec{nullptr, nullptr};
+}
+
+size_t WSSendBatch::Flush(Sink sink, void* user)
+{
+    if (_flushing || _desc.empty())
+        return 0;
+    if (_desc.size() > UINT32_MAX)
+        throw std::length_error("WSSendBatch: more than 2^32-1 frames in one flush");
+    _flushing = true;
+    struct Done {
+        WSSendBatch* t;
+        ~Done() { t->_flushing = false; }
+    } done{this};
+    const uint32_t n = uint32_t(_desc.size());
+    uint64_t total = 0;
+    for (const wsg_send_desc& d : _desc)
+        total += wsg_frame_size(d.opcode, d.mask, d.len, d.status);
+    grow_pinned(_wire.p, _wire.cap, 0, std::max<uint64_t>(total, 1));
+    _wire_off.resize(size_t(n) + 1);
+    check(wsg_encode_batch_host(_ctx ? _ctx : ThreadCodec(), _payload.p, _payload.len, _desc.data(), n, _wire.p,
+                                _wire.cap, _wire_off.data()),
+          "wsg_encode_batch_host");
+    // encoded: the queue is empty again before any frame is handed out, so a
+    // transport's SendAsync may queue more frames (they go with the next
+    // flush); if the encode failed above, everything stays queued
+    std::vector<Rec> recs;
+    recs.swap(_recs);
+    _desc.clear();
+    _payload.len = 0;
+    size_t sent = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t* f = _wire.p + _wire_off[i];
+        const size_t len = size_t(_wire_off[i + 1] - _wire_off[i]);
+        if (recs[i].transport) {
+            recs[i].transport->SendAsync(f, len);
+            ++sent;
+        } else if (recs[i].tag && sink) {
+            sink(user, recs[i].tag, f, len);
+            ++sent;
+        }
+    }
+    return sent;
+}
+
 } // namespace WS
 } // namespace CppServer
 
@@ -303,6 +423,92 @@ int wsg_rx_flush(wsg_rx* rx, wsg_rx_cb cb, void* user, uint32_t* delivered)
     g_rx_dispatch = saved;
     if (delivered)
         *delivered = uint32_t(n);
+    return rc;
+}
+
+// ---- batched send ---------------------------------------------------------
+
+struct wsg_tx {
+    explicit wsg_tx(wsg_ctx* c) : batch(c) {}
+    CppServer::WS::WSSendBatch batch;
+};
+
+int wsg_tx_create(wsg_ctx* ctx, wsg_tx** out)
+{
+    if (!ctx || !out)
+        return WSG_EINVAL;
+    *out = new (std::nothrow) wsg_tx(ctx);
+    return *out ? WSG_OK : WSG_ENOMEM;
+}
+
+int wsg_tx_destroy(wsg_tx* tx)
+{
+    if (!tx)
+        return WSG_EINVAL;
+    delete tx;
+    return WSG_OK;
+}
+
+int wsg_tx_queue(wsg_tx* tx, wsg_session* s, uint8_t opcode, int mask, const void* buf, size_t size, int32_t status)
+{
+    if (!tx || !s || (size && !buf))
+        return WSG_EINVAL;
+    try {
+        std::scoped_lock locker(s->send_lock());   // the key is read under the send lock, as Send* does
+        tx->batch.Queue(static_cast<void*>(s), s->send_key(), opcode, mask != 0, buf, size, status);
+        return WSG_OK;
+    } catch (...) {
+        return WSG_ENOMEM;
+    }
+}
+
+int wsg_tx_forget(wsg_tx* tx, wsg_session* s)
+{
+    if (!tx || !s)
+        return WSG_EINVAL;
+    tx->batch.Forget(static_cast<void*>(s));
+    return WSG_OK;
+}
+
+int wsg_tx_pending(wsg_tx* tx, uint32_t* frames, uint64_t* payload_bytes)
+{
+    if (!tx)
+        return WSG_EINVAL;
+    if (frames)
+        *frames = uint32_t(tx->batch.frames());
+    if (payload_bytes)
+        *payload_bytes = tx->batch.payload_bytes();
+    return WSG_OK;
+}
+
+namespace {
+struct TxSink {
+    wsg_tx_sink sink;
+    void* user;
+};
+void tx_sink(void* user, void* tag, const uint8_t* frame, size_t size)
+{
+    const TxSink* t = static_cast<const TxSink*>(user);
+    t->sink(t->user, static_cast<wsg_session*>(tag), frame, size);
+}
+} // namespace
+
+int wsg_tx_flush(wsg_tx* tx, wsg_tx_sink sink, void* user, uint32_t* sent)
+{
+    if (!tx || !sink)
+        return WSG_EINVAL;
+    TxSink t{sink, user};
+    size_t n = 0;
+    int rc = WSG_OK;
+    try {
+        n = tx->batch.Flush(tx_sink, &t);
+    } catch (const std::bad_alloc&) {
+        rc = WSG_ENOMEM;
+    } catch (...) {
+        rc = WSG_EHIP;
+    }
+    if (sent)
+        *sent = uint32_t(n);
     return rc;
 }
 

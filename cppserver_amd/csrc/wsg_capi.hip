@@ -10,6 +10,17 @@
 #include <new>
 #include <vector>
 
+// Encode scratch (scan partials, piece starts, piece -> frame map); the ctx
+// has one for wsg_encode_batch and every pipeline slot its own.
+struct wsg_enc_scratch {
+    uint64_t* d_scan = nullptr;          // sums | piece sums | prefixes | piece prefixes
+    uint64_t scan_cap = 0;               // entries
+    uint32_t* d_piece_start = nullptr;   // n + 1 piece starts
+    uint64_t piece_start_cap = 0;
+    uint32_t* d_piece_frame = nullptr;   // piece -> frame
+    uint64_t piece_frame_cap = 0;
+};
+
 struct wsg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -19,12 +30,7 @@ struct wsg_ctx {
     // scratch
     uint32_t* d_tiles = nullptr;
     uint64_t tiles_cap = 0;
-    uint64_t* d_scan = nullptr;     // encode scan: sums | piece sums | prefixes | piece prefixes
-    uint64_t scan_cap = 0;          // blocks per quarter
-    uint32_t* d_piece_start = nullptr;   // encode: n + 1 piece starts
-    uint64_t piece_start_cap = 0;
-    uint32_t* d_piece_frame = nullptr;   // encode: piece -> frame
-    uint64_t piece_frame_cap = 0;
+    wsg_enc_scratch enc;
     // staging for host entry points
     uint8_t* d_stage = nullptr;
     uint8_t* h_stage = nullptr;
@@ -48,6 +54,16 @@ struct wsg_ctx {
         uint64_t frames_cap = 0;
         uint32_t* d_tiles = nullptr;
         uint64_t tiles_cap = 0;
+        // encode (wsg_encode_batch_host): payload in, frames out in d_wire
+        uint8_t* d_payload = nullptr;
+        uint64_t payload_cap = 0;
+        wsg_send_desc* d_desc = nullptr;
+        uint64_t desc_cap = 0;
+        wsg_send_desc* h_desc = nullptr;  // rebased descriptors (pinned)
+        uint64_t h_desc_cap = 0;
+        uint64_t* d_woff = nullptr;
+        uint64_t woff_cap = 0;
+        wsg_enc_scratch enc;
         // work to finish on the host once `done` has fired
         bool busy = false;
         uint8_t* out_dst = nullptr;      // pageable destination of h_out (null: DMA'd directly)
@@ -106,20 +122,12 @@ int ensure_tiles(wsg_ctx* c, uint64_t tiles)
     return WSG_OK;
 }
 
-int ensure_scan(wsg_ctx* c, uint64_t blocks)
+void free_enc(wsg_enc_scratch& e)
 {
-    blocks = std::max<uint64_t>(blocks, 1);
-    if (blocks <= c->scan_cap)
-        return WSG_OK;
-    WSG_HIP(hipDeviceSynchronize());
-    if (c->d_scan)
-        WSG_HIP(hipFree(c->d_scan));
-    c->d_scan = nullptr;
-    c->scan_cap = 0;
-    if (hipMalloc(&c->d_scan, 4 * blocks * sizeof(uint64_t)) != hipSuccess)
-        return WSG_ENOMEM;
-    c->scan_cap = blocks;
-    return WSG_OK;
+    (void)hipFree(e.d_scan);
+    (void)hipFree(e.d_piece_start);
+    (void)hipFree(e.d_piece_frame);
+    e = wsg_enc_scratch{};
 }
 
 // grow a device array of T to at least `want` entries
@@ -286,9 +294,7 @@ int wsg_destroy(wsg_ctx* c)
     }
     (void)hipFree(c->d_err);
     (void)hipFree(c->d_tiles);
-    (void)hipFree(c->d_scan);
-    (void)hipFree(c->d_piece_start);
-    (void)hipFree(c->d_piece_frame);
+    free_enc(c->enc);
     (void)hipFree(c->d_stage);
     (void)hipFree(c->d_fs);
     (void)hipFree(c->d_info);
@@ -299,6 +305,12 @@ int wsg_destroy(wsg_ctx* c)
             (void)hipStreamSynchronize(sl.stream);
         (void)hipFree(sl.d_wire);
         (void)hipFree(sl.d_tiles);
+        (void)hipFree(sl.d_payload);
+        (void)hipFree(sl.d_desc);
+        (void)hipFree(sl.d_woff);
+        if (sl.h_desc)
+            (void)hipHostFree(sl.h_desc);
+        free_enc(sl.enc);
         (void)hipFree(sl.d_fs);
         (void)hipFree(sl.d_info);
         if (sl.h_in)
@@ -374,6 +386,35 @@ int wsg_decode_batch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const
     return decode_launch(c, d_wire, wire_len, d_frame_start, n, d_out, d_info, c->d_tiles, pick(c, stream));
 }
 
+namespace {
+
+// upper bound of the pieces: sum of ceil((size + 15) / PIECE) over frames
+inline uint64_t pieces_bound(uint32_t n, uint64_t wire_cap) { return wire_cap / wsg::PIECE + 2 * uint64_t(n) + 1; }
+
+int ensure_enc(wsg_enc_scratch& e, uint32_t n, uint64_t wire_cap)
+{
+    if (int rc = ensure_array(e.d_scan, e.scan_cap, 4 * ceil_div(n, wsg::SCAN_ITEMS)))
+        return rc;
+    if (int rc = ensure_array(e.d_piece_start, e.piece_start_cap, uint64_t(n) + 1))
+        return rc;
+    return ensure_array(e.d_piece_frame, e.piece_frame_cap, pieces_bound(n, wire_cap));
+}
+
+int encode_launch(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, const wsg_send_desc* d_desc, uint32_t n,
+                  uint8_t* d_wire, uint64_t wire_cap, uint64_t* d_wire_off, wsg_enc_scratch& e)
+{
+    const uint64_t pieces_cap = pieces_bound(n, wire_cap);
+    WSG_HIP(wsg::launch_encode_scan(s, d_desc, n, d_wire_off, e.d_piece_start, e.d_scan, e.d_piece_frame, pieces_cap,
+                                    wire_cap, c->d_err));
+    const int t = timing_begin(c, s);
+    WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, ceil_div(pieces_cap, wsg::BLOCK / 64)), d_payload, d_desc, n,
+                                    d_wire_off, e.d_piece_start, e.d_piece_frame, d_wire, wire_cap));
+    timing_end(c, s, t);
+    return WSG_OK;
+}
+
+} // namespace
+
 int wsg_encode_batch(wsg_ctx* c, const uint8_t* d_payload, const wsg_send_desc* d_desc, uint32_t n, uint8_t* d_wire,
                      uint64_t wire_cap, uint64_t* d_wire_off, void* stream)
 {
@@ -386,22 +427,9 @@ int wsg_encode_batch(wsg_ctx* c, const uint8_t* d_payload, const wsg_send_desc* 
         WSG_HIP(hipMemsetAsync(d_wire_off, 0, sizeof(uint64_t), s));
         return WSG_OK;
     }
-    // upper bound of the pieces: sum of ceil((size + 15) / PIECE) over frames
-    const uint64_t pieces_cap = wire_cap / wsg::PIECE + 2 * uint64_t(n) + 1;
-    const uint64_t nb = ceil_div(n, wsg::SCAN_ITEMS);
-    if (int rc = ensure_scan(c, nb))
+    if (int rc = ensure_enc(c->enc, n, wire_cap))
         return rc;
-    if (int rc = ensure_array(c->d_piece_start, c->piece_start_cap, uint64_t(n) + 1))
-        return rc;
-    if (int rc = ensure_array(c->d_piece_frame, c->piece_frame_cap, pieces_cap))
-        return rc;
-    WSG_HIP(wsg::launch_encode_scan(s, d_desc, n, d_wire_off, c->d_piece_start, c->d_scan, c->d_piece_frame,
-                                    pieces_cap, wire_cap, c->d_err));
-    const int t = timing_begin(c, s);
-    WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, ceil_div(pieces_cap, wsg::BLOCK / 64)), d_payload, d_desc, n,
-                                    d_wire_off, c->d_piece_start, c->d_piece_frame, d_wire, wire_cap));
-    timing_end(c, s, t);
-    return WSG_OK;
+    return encode_launch(c, s, d_payload, d_desc, n, d_wire, wire_cap, d_wire_off, c->enc);
 }
 
 int wsg_fanout_encode(wsg_ctx* c, const uint8_t* d_payload, uint64_t len, const uint32_t* d_keys, uint32_t k,
@@ -640,6 +668,170 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
             first = r.error;
     }
     return first;
+}
+
+namespace {
+
+int slot_reserve_enc(wsg_ctx::Slot& sl, uint64_t payload_bytes, uint64_t wire_bytes, uint32_t frames,
+                     bool need_host)
+{
+    if (!sl.stream) {
+        WSG_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+        WSG_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    }
+    if (int rc = ensure_array(sl.d_payload, sl.payload_cap, payload_bytes + 32))
+        return rc;
+    if (int rc = ensure_array(sl.d_wire, sl.wire_cap, wire_bytes + 32))
+        return rc;
+    if (int rc = ensure_array(sl.d_desc, sl.desc_cap, frames))
+        return rc;
+    if (int rc = ensure_array(sl.d_woff, sl.woff_cap, uint64_t(frames) + 1))
+        return rc;
+    if (int rc = ensure_enc(sl.enc, frames, wire_bytes))
+        return rc;
+    if (frames > sl.h_desc_cap) {
+        if (sl.h_desc)
+            (void)hipHostFree(sl.h_desc);
+        sl.h_desc = nullptr;
+        sl.h_desc_cap = 0;
+        if (hipHostMalloc(&sl.h_desc, frames * sizeof(wsg_send_desc), hipHostMallocDefault) != hipSuccess)
+            return WSG_ENOMEM;
+        sl.h_desc_cap = frames;
+    }
+    const uint64_t host = std::max(payload_bytes, wire_bytes) + 32;
+    if (need_host && host > sl.host_cap) {
+        if (sl.h_in)
+            (void)hipHostFree(sl.h_in);
+        if (sl.h_out)
+            (void)hipHostFree(sl.h_out);
+        sl.h_in = sl.h_out = nullptr;
+        sl.host_cap = 0;
+        if (hipHostMalloc(&sl.h_in, host, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(&sl.h_out, host, hipHostMallocDefault) != hipSuccess)
+            return WSG_ENOMEM;
+        sl.host_cap = host;
+    }
+    return WSG_OK;
+}
+
+} // namespace
+
+int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_len, const wsg_send_desc* desc,
+                          uint32_t n, uint8_t* wire, uint64_t wire_cap, uint64_t* wire_off)
+{
+    if (!c || !wire_off || (n && (!desc || !wire)) || (payload_len && !payload))
+        return WSG_EINVAL;
+    // frame offsets on the host (the same arithmetic as k_encode_scan_*), so
+    // that segments can be cut and copied back without a device round trip
+    wire_off[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const wsg_send_desc& d = desc[i];
+        if (d.len > payload_len || d.src_off > payload_len - d.len)
+            return WSG_EINVAL;
+        wire_off[i + 1] = wire_off[i] + wsg_frame_size(d.opcode, d.mask, d.len, d.status);
+    }
+    if (wire_off[n] > wire_cap)
+        return WSG_ENOMEM;
+    if (n == 0)
+        return WSG_OK;
+    uint64_t seg_bytes = 32ull << 20;
+    if (const char* e = std::getenv("WSG_STAGE_MB"))
+        seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+    const bool in_pinned = host_pinned(payload), out_pinned = host_pinned(wire);
+
+    // segments of whole frames, ~seg_bytes of wire each
+    struct Seg {
+        uint32_t i0, i1;
+        uint64_t lo, hi;   // payload source range [lo, hi) (16-B aligned lo)
+        uint64_t sum;      // payload bytes of its frames
+        bool gather;       // frames' payloads not one tight range: copy them together
+    };
+    std::vector<Seg> segs;
+    for (uint32_t i0 = 0; i0 < n;) {
+        Seg g{i0, i0, ~uint64_t(0), 0, 0, false};
+        do {
+            const wsg_send_desc& d = desc[g.i1];
+            if (d.len) {
+                g.lo = std::min(g.lo, d.src_off);
+                g.hi = std::max(g.hi, d.src_off + d.len);
+            }
+            g.sum += d.len;
+            ++g.i1;
+        } while (g.i1 < n && wire_off[g.i1] - wire_off[i0] < seg_bytes);
+        if (g.lo > g.hi)
+            g.lo = g.hi = 0;
+        g.lo &= ~uint64_t(15);
+        g.gather = g.hi - g.lo > g.sum + 16 * uint64_t(g.i1 - g.i0) + 4096;
+        segs.push_back(g);
+        i0 = g.i1;
+    }
+    uint64_t max_payload = 0, max_wire = 0;
+    uint32_t max_frames = 0;
+    bool need_host = !out_pinned;
+    for (const Seg& g : segs) {
+        max_payload = std::max(max_payload, g.gather ? g.sum : g.hi - g.lo);
+        max_wire = std::max(max_wire, wire_off[g.i1] - wire_off[g.i0]);
+        max_frames = std::max(max_frames, g.i1 - g.i0);
+        need_host = need_host || g.gather || !in_pinned;
+    }
+    for (auto& sl : c->slots)
+        if (int rc = slot_reserve_enc(sl, max_payload, max_wire, max_frames, need_host))
+            return rc;
+
+    for (size_t k = 0; k < segs.size(); ++k) {
+        const Seg& g = segs[k];
+        wsg_ctx::Slot& sl = c->slots[k % wsg_ctx::kSlots];
+        if (int rc = slot_drain(sl))
+            return rc;
+        const uint32_t m = g.i1 - g.i0;
+        const uint8_t* src = payload + g.lo;
+        uint64_t plen = g.hi - g.lo;
+        if (g.gather) {
+            uint64_t at = 0;
+            for (uint32_t j = 0; j < m; ++j) {
+                wsg_send_desc d = desc[g.i0 + j];
+                if (d.len)
+                    std::memcpy(sl.h_in + at, payload + d.src_off, d.len);
+                d.src_off = at;
+                sl.h_desc[j] = d;
+                at += d.len;
+            }
+            src = sl.h_in;
+            plen = at;
+        } else {
+            for (uint32_t j = 0; j < m; ++j) {
+                wsg_send_desc d = desc[g.i0 + j];
+                d.src_off = d.len ? d.src_off - g.lo : 0;
+                sl.h_desc[j] = d;
+            }
+            if (!in_pinned && plen) {
+                std::memcpy(sl.h_in, src, plen);
+                src = sl.h_in;
+            }
+        }
+        if (plen)
+            WSG_HIP(hipMemcpyAsync(sl.d_payload, src, plen, hipMemcpyHostToDevice, sl.stream));
+        WSG_HIP(hipMemcpyAsync(sl.d_desc, sl.h_desc, m * sizeof(wsg_send_desc), hipMemcpyHostToDevice, sl.stream));
+        const uint64_t wlen = wire_off[g.i1] - wire_off[g.i0];
+        if (int rc = encode_launch(c, sl.stream, sl.d_payload, sl.d_desc, m, sl.d_wire, wlen, sl.d_woff, sl.enc))
+            return rc;
+        if (out_pinned) {
+            WSG_HIP(hipMemcpyAsync(wire + wire_off[g.i0], sl.d_wire, wlen, hipMemcpyDeviceToHost, sl.stream));
+            sl.out_dst = nullptr;
+        } else {
+            WSG_HIP(hipMemcpyAsync(sl.h_out, sl.d_wire, wlen, hipMemcpyDeviceToHost, sl.stream));
+            sl.out_dst = wire + wire_off[g.i0];
+            sl.out_src = 0;
+        }
+        sl.out_len = wlen;
+        sl.info_n = 0;
+        WSG_HIP(hipEventRecord(sl.done, sl.stream));
+        sl.busy = true;
+    }
+    for (auto& sl : c->slots)
+        if (int rc = slot_drain(sl))
+            return rc;
+    return wsg_sync(c, nullptr);   // capacity was checked above; anything latched is a real error
 }
 
 uint64_t wsg_frame_size(uint8_t opcode, int mask, uint64_t len, int32_t status)

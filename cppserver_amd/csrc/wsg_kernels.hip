@@ -49,6 +49,9 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_DIAG
 #define WSG_DIAG 0   // 1/2: timing-only diagnostic builds of k_decode_unmask (tools/)
 #endif
+#ifndef WSG_DIAG_FAN
+#define WSG_DIAG_FAN 0   // timing-only fan-out diagnostics: 1 no key loads, 2 no payload loads, 4 stores only
+#endif
 #ifndef WSG_NT_STORE
 #define WSG_NT_STORE 1
 #endif
@@ -879,69 +882,216 @@ __device__ __forceinline__ uint32_t fan_byte(const uint8_t* __restrict__ payload
     return uint32_t(payload[k - g.prefix]) ^ key_byte(key, k);
 }
 
+// 16 payload bytes as seen from a chunk: byte j = payload[c + j] where that
+// offset is inside [0, len) (else 0).  Reads only aligned 16-B blocks that
+// hold a wanted byte, at most two.
+__device__ __forceinline__ v4u fan_window(const uint8_t* __restrict__ payload, uint64_t len, int64_t c)
+{
+    const intptr_t base = reinterpret_cast<intptr_t>(payload);
+    const intptr_t b = base + intptr_t(c);
+    const uint32_t s = uint32_t(b & 15);
+    const intptr_t a0 = b - intptr_t(s);
+    const intptr_t lo_valid = base, hi_valid = base + intptr_t(len);
+    v4u lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
+    if (a0 < hi_valid && a0 + 16 > lo_valid)
+        lo = ld16(reinterpret_cast<const uint8_t*>(a0));
+    if (s != 0 && a0 + 16 < hi_valid && a0 + 32 > lo_valid)
+        hi = ld16(reinterpret_cast<const uint8_t*>(a0 + 16));
+    return s ? funnel(lo, hi, s) : lo;
+}
+
+// 128-bit byte shifts and byte masks (runtime counts) built on funnel().
+__device__ __forceinline__ v4u shr_bytes(v4u x, uint64_t o)   // byte j = x[j + o]
+{
+    return o >= CHUNK ? v4u{0, 0, 0, 0} : funnel(x, v4u{0, 0, 0, 0}, uint32_t(o));
+}
+__device__ __forceinline__ v4u shl_bytes(v4u x, uint64_t s)   // byte j = x[j - s]
+{
+    return s == 0 ? x : s >= CHUNK ? v4u{0, 0, 0, 0} : funnel(v4u{0, 0, 0, 0}, x, uint32_t(CHUNK - s));
+}
+__device__ __forceinline__ v4u low_bytes(uint64_t n)   // bytes [0, n) = 0xFF
+{
+    const uint64_t lo = n >= 8 ? ~uint64_t(0) : (uint64_t(1) << (8 * n)) - 1;
+    const uint64_t hi = n >= 16 ? ~uint64_t(0) : n <= 8 ? 0 : (uint64_t(1) << (8 * (n - 8))) - 1;
+    return v4u{uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32)};
+}
+
+// Frames of one fan-out differ only in their key: the header + status bytes
+// (data0 <= 16 of them) are a constant vector plus the key bytes.
+struct FanGeom {
+    SendGeom g;
+    uint32_t data0;   // frame offset of the first payload byte (<= 16)
+    uint32_t kpos;    // frame offset of the mask key (2 + ext)
+    bool mask;
+    v4u hp0;          // header with the key bytes left 0; status bytes 0
+};
+
+__device__ __forceinline__ FanGeom fan_geom(uint8_t opcode, bool mask, uint64_t len)
+{
+    FanGeom f;
+    f.g = send_geom(opcode, mask, len, 0);
+    f.data0 = f.g.hdr + f.g.prefix;
+    f.kpos = f.g.hdr - (mask ? 4u : 0u);
+    f.mask = mask;
+    f.hp0 = v4u{0, 0, 0, 0};
+#pragma unroll 1
+    for (uint32_t r = 0; r < f.kpos; ++r)
+        put_byte(f.hp0, r, header_byte(opcode, mask, f.g.body, 0, r));
+    return f;
+}
+
+// Bytes [o, o + 16) of the frame with key `key` (bytes past the frame are 0).
+__device__ __forceinline__ v4u fan_frame_bytes(const uint8_t* __restrict__ payload, uint64_t len, const FanGeom& f,
+                                               uint64_t fsize, uint32_t key, uint64_t o)
+{
+    v4u hp = f.hp0;
+    if (f.mask)
+        hp |= shl_bytes(v4u{key, 0, 0, 0}, f.kpos);
+    if (f.g.prefix)
+        hp |= shl_bytes(v4u{key & 0xFFFFu, 0, 0, 0}, f.g.hdr);   // status 0 ^ key
+    v4u out = shr_bytes(hp, o);
+    const uint64_t lo = o < f.data0 ? f.data0 - o : 0;               // chunk bytes [lo, hi) are payload
+    const uint64_t hi = fsize - o < CHUNK ? fsize - o : CHUNK;
+    if (lo < hi) {
+        const v4u w = fan_window(payload, len, int64_t(o) - int64_t(f.data0));
+        const v4u m = low_bytes(hi) & ~low_bytes(lo);
+        out |= (w ^ key_rot(key, uint32_t(o - f.g.hdr))) & m;
+    }
+    return out;
+}
+
+// Grid = `main_blocks` streaming blocks, then the edge blocks.
+//  * Streaming waves own 64 x FU consecutive chunks and write every chunk
+//    that is all payload of one frame (the frame index comes from one scalar
+//    division per pass when frames are >= 1 KiB, else a per-lane reciprocal).
+//  * Edge lanes own one (frame f, header chunk h) item each and write the
+//    chunk(s) that hold frame f's start / header / status bytes, built from
+//    frame f - 1's tail and frame f's head.  A chunk is written by exactly
+//    one side (identical bytes if two edge items meet on one chunk), so the
+//    streaming waves never branch into the header code.
+//  * Frames shorter than a chunk: the streaming waves do every chunk byte by
+//    byte and there are no edge blocks.
+__device__ __forceinline__ void fan_locate(uint64_t p, uint64_t fsize, double inv, uint64_t& i, uint64_t& r)
+{
+    i = uint64_t(double(p) * inv);
+    int64_t rr = int64_t(p - i * fsize);
+    if (rr < 0) {
+        --i;
+        rr += int64_t(fsize);
+    } else if (uint64_t(rr) >= fsize) {
+        ++i;
+        rr -= int64_t(fsize);
+    }
+    r = uint64_t(rr);
+}
+
+__device__ __forceinline__ void fan_store(uint8_t* __restrict__ wire, uint64_t c, uint64_t chunks, uint64_t total,
+                                          v4u w)
+{
+    if (c + 1 < chunks || (total & (CHUNK - 1)) == 0) {
+        st16nt(wire + c * CHUNK, w);
+    } else {
+#pragma unroll 1
+        for (uint32_t j = 0; j < (total & (CHUNK - 1)); ++j)
+            wire[c * CHUNK + j] = uint8_t(lane_byte(w, j));
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_fanout_flat(const uint8_t* __restrict__ payload, uint64_t len,
                                                        const uint32_t* __restrict__ keys, uint32_t k, uint8_t opcode,
-                                                       uint32_t mask, uint64_t fsize, double inv,
+                                                       uint32_t mask, uint64_t fsize, double inv, uint32_t main_blocks,
                                                        uint8_t* __restrict__ wire)
 {
-    const SendGeom g = send_geom(opcode, mask != 0, len, 0);
+    const FanGeom f = fan_geom(opcode, mask != 0, len);
+    const SendGeom& g = f.g;
     const uint64_t total = fsize * k;
     const uint64_t chunks = (total + CHUNK - 1) / CHUNK;
-    const uint64_t data0 = g.hdr + g.prefix;   // frame offset of the first payload byte
+    const uint64_t data0 = f.data0;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t step = uint64_t(gridDim.x) * (BLOCK / 64) * (64 * FU);
+
+    if (blockIdx.x >= main_blocks) {
+        // edge items: 2 per frame start (the last "start" is the wire's end)
+        const uint64_t item = uint64_t(blockIdx.x - main_blocks) * BLOCK + threadIdx.x;
+        const uint64_t fr = item >> 1, h = item & 1;
+        if (fr > k)
+            return;
+        const uint64_t start = fr * fsize;
+        const uint64_t c = start / CHUNK + h;
+        if (c >= chunks || (h && (start & (CHUNK - 1)) + data0 <= CHUNK) || (fr == k && h))
+            return;
+        uint64_t i, r;
+        fan_locate(c * CHUNK, fsize, inv, i, r);
+        v4u w = fan_frame_bytes(payload, len, f, fsize, keys[i], r);
+        const uint64_t split = fsize - r;
+        if (split < CHUNK && i + 1 < k)
+            w |= shl_bytes(fan_frame_bytes(payload, len, f, fsize, keys[i + 1], 0), split);
+        fan_store(wire, c, chunks, total, w);
+        return;
+    }
+
+    const uint64_t step = uint64_t(main_blocks) * (BLOCK / 64) * (64 * FU);
+    const bool big = fsize >= uint64_t(64) * CHUNK;   // a 1 KiB pass row spans at most 2 frames
     for (uint64_t base = (uint64_t(blockIdx.x) * (BLOCK / 64) + wave_id()) * (64 * FU); base < chunks; base += step) {
-        v4u v[FU];
-#pragma unroll
-        for (int u = 0; u < FU; ++u) {
-            const uint64_t c = base + uint64_t(u) * 64 + lane;
-            v[u] = v4u{0, 0, 0, 0};
-            if (c >= chunks)
-                continue;
-            const uint64_t p = c * CHUNK;
-            uint64_t i = uint64_t(double(p) * inv);
-            int64_t r = int64_t(p - i * fsize);
-            if (r < 0) {
-                --i;
-                r += int64_t(fsize);
-            } else if (uint64_t(r) >= fsize) {
-                ++i;
-                r -= int64_t(fsize);
-            }
-            if (uint64_t(r) >= data0 && uint64_t(r) + CHUNK <= fsize) {
-                // all payload bytes of frame i
-                const uint64_t o = uint64_t(r) - data0;
-                const uintptr_t a = reinterpret_cast<uintptr_t>(payload) + o;
-                const uint32_t s = uint32_t(a & 15u);
-                const uint8_t* a0 = reinterpret_cast<const uint8_t*>(a - s);
-                const v4u lo = ld16(a0);
-                const v4u d = s ? funnel(lo, ld16(a0 + CHUNK), s) : lo;
-                v[u] = d ^ key_rot(keys[i], uint32_t(uint64_t(r) - g.hdr));
-            } else {
-                // header / status bytes, or a frame boundary inside the chunk
-                uint64_t ii = i, rr = uint64_t(r);
-#pragma unroll
-                for (uint32_t j = 0; j < CHUNK; ++j) {
-                    while (rr >= fsize) {
-                        rr -= fsize;
-                        ++ii;
+        if (fsize < CHUNK) {
+            // several frames per chunk: byte by byte
+#pragma unroll 1
+            for (int u = 0; u < FU; ++u) {
+                const uint64_t c = base + uint64_t(u) * 64 + lane;
+                if (c >= chunks)
+                    break;
+                uint64_t i, r;
+                fan_locate(c * CHUNK, fsize, inv, i, r);
+                v4u e = {0, 0, 0, 0};
+#pragma unroll 1
+                for (uint32_t j = 0; j < CHUNK; ++j, ++r) {
+                    while (r >= fsize) {
+                        r -= fsize;
+                        ++i;
                     }
-                    if (ii < k)
-                        put_byte(v[u], j, fan_byte(payload, keys, opcode, mask != 0, g, fsize, ii, rr));
-                    ++rr;
+                    if (i < k)
+                        put_byte(e, j, fan_byte(payload, keys, opcode, mask != 0, g, fsize, i, r));
                 }
+                fan_store(wire, c, chunks, total, e);
             }
+            continue;
+        }
+        v4u v[FU];
+        bool fast[FU];
+        uint64_t i0 = 0, r0 = 0;
+        if (big) {
+            // frame of the pass row's first chunk: one scalar division per row
+            i0 = __builtin_amdgcn_readfirstlane(uint32_t((base * CHUNK) / fsize));
+            r0 = base * CHUNK - i0 * fsize;
         }
 #pragma unroll
         for (int u = 0; u < FU; ++u) {
             const uint64_t c = base + uint64_t(u) * 64 + lane;
-            if (c + 1 < chunks || (c + 1 == chunks && (total & (CHUNK - 1)) == 0)) {
-                st16nt(wire + c * CHUNK, v[u]);
-            } else if (c + 1 == chunks) {
-                for (uint32_t j = 0; j < (total & (CHUNK - 1)); ++j)
-                    wire[c * CHUNK + j] = uint8_t(lane_byte(v[u], j));
+            uint64_t i, r;
+            if (big) {
+                // row u starts at most (FU - 1) KiB + r0 past frame i0's start
+                r = r0 + (uint64_t(u) * 64 + lane) * CHUNK;
+                i = i0;
+#pragma unroll
+                for (int q = 0; q < FU + 1; ++q)
+                    if (r >= fsize) {
+                        r -= fsize;
+                        ++i;
+                    }
+            } else {
+                fan_locate(c * CHUNK, fsize, inv, i, r);
+            }
+            fast[u] = c < chunks && r >= data0 && r + CHUNK <= fsize;
+            v[u] = v4u{0, 0, 0, 0};
+            if (fast[u]) {
+                const v4u d = (WSG_DIAG_FAN & 2) ? v4u{uint32_t(r), 1, 2, 3}
+                                                 : fan_window(payload, len, int64_t(r) - int64_t(data0));
+                v[u] = d ^ key_rot((WSG_DIAG_FAN & 1) ? uint32_t(i) : keys[i], uint32_t(r - g.hdr));
             }
         }
+#pragma unroll
+        for (int u = 0; u < FU; ++u)
+            if (fast[u])
+                st16nt(wire + (base + uint64_t(u) * 64 + lane) * CHUNK, v[u]);
     }
 }
 
@@ -1009,7 +1159,13 @@ hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64
                          uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire)
 {
     if (fanout_flat)
-        k_fanout_flat<<<grid, BLOCK, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, 1.0 / double(fsize), wire);
+    {
+        // edge blocks: two items per frame start (k + 1 starts); none for
+        // frames shorter than a chunk (the streaming waves do those)
+        const uint64_t edge_blocks = fsize >= CHUNK ? (2 * (uint64_t(k) + 1) + BLOCK - 1) / BLOCK : 0;
+        k_fanout_flat<<<dim3(uint32_t(grid + edge_blocks)), BLOCK, 0, s>>>(
+            payload, len, keys, k, opcode, mask, fsize, 1.0 / double(fsize), uint32_t(grid), wire);
+    }
     else
         k_fanout<<<grid, BLOCK, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, wire);
     return hipGetLastError();

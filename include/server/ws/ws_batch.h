@@ -87,6 +87,67 @@ private:
     bool _flushing = false;
 };
 
+class Transport;
+
+/*
+ * Batched send for many connections.  The reference
+ * encodes every Send*Async on the caller's thread (PrepareSendFrame,
+ * ws.cpp:212-271) and hands the frame to the transport right away
+ * (tcp_session.cpp:257-307).  Queue() records the same call — the
+ * connection's key, opcode, mask flag, close status and a copy of the
+ * payload — and Flush() encodes every queued frame in one pipelined GPU pass
+ * (wsg_encode_batch_host) and hands each frame to its transport in queue
+ * order: the same bytes the per-call path sends, in the same order per
+ * connection.
+ */
+class WSSendBatch
+{
+public:
+    //! Sink for frames queued without a transport (the C-ABI's wsg_tx_flush)
+    using Sink = void (*)(void* user, void* tag, const uint8_t* frame, size_t size);
+
+    explicit WSSendBatch(wsg_ctx* codec = nullptr);
+    ~WSSendBatch();
+    WSSendBatch(const WSSendBatch&) = delete;
+    WSSendBatch& operator=(const WSSendBatch&) = delete;
+
+    //! PrepareSendFrame(opcode, mask, buffer, size, status) with send key
+    //! `key`, deferred: the frame goes to transport.SendAsync at Flush()
+    void Queue(Transport& transport, uint32_t key, uint8_t opcode, bool mask, const void* buffer, size_t size,
+               int status = 0);
+    //! The same, for a frame the flush sink receives with `tag`
+    void Queue(void* tag, uint32_t key, uint8_t opcode, bool mask, const void* buffer, size_t size, int status = 0);
+    //! Drop every queued frame of `transport` (call before destroying it)
+    void Forget(Transport& transport);
+    //! Drop every queued frame queued with `tag`
+    void Forget(void* tag);
+    //! Encode everything queued and hand the frames out in queue order;
+    //! returns the number of frames handed out
+    size_t Flush(Sink sink = nullptr, void* user = nullptr);
+
+    size_t frames() const { return _desc.size(); }
+    uint64_t payload_bytes() const { return _payload.len; }
+
+private:
+    struct Pinned {
+        uint8_t* p = nullptr;
+        uint64_t cap = 0, len = 0;
+    };
+    struct Rec {
+        Transport* transport;
+        void* tag;
+    };
+    void Push(Transport* t, void* tag, uint32_t key, uint8_t opcode, bool mask, const void* buffer, size_t size,
+              int status);
+
+    wsg_ctx* _ctx;
+    Pinned _payload, _wire;
+    std::vector<wsg_send_desc> _desc;
+    std::vector<Rec> _recs;
+    std::vector<uint64_t> _wire_off;
+    bool _flushing = false;
+};
+
 } // namespace WS
 } // namespace CppServer
 

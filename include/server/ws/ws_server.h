@@ -22,7 +22,11 @@ class WSServer : protected WebSocket
 {
 public:
     explicit WSServer(wsg_ctx* codec = nullptr) : WebSocket(codec) {}
-    virtual ~WSServer() { EnableBatchReceive(false); }
+    virtual ~WSServer()
+    {
+        EnableBatchReceive(false);
+        EnableBatchSend(false);
+    }
 
     //! Register / unregister a connected session (the reference's TCPServer session map)
     void AddSession(const std::shared_ptr<WSSession>& session);
@@ -53,10 +57,18 @@ public:
     //! flush; returns the number of frames delivered
     size_t FlushReceived();
 
+    //! Batched send: the sessions' Send*Async frames
+    //! are encoded in one GPU pass per FlushSend() and handed to their
+    //! transports in queue order.  Multicast* flushes it first (order).
+    void EnableBatchSend(bool on);
+    bool IsBatchSend() const { return _tx_batch != nullptr; }
+    size_t FlushSend();
+
 private:
     size_t MulticastFrame(uint8_t opcode, const void* buffer, size_t size);
 
     std::unique_ptr<WSReceiveBatch> _rx_batch;
+    std::unique_ptr<WSSendBatch> _tx_batch;
 
     mutable std::shared_mutex _sessions_lock;
     std::vector<std::shared_ptr<WSSession>> _sessions;

@@ -68,6 +68,10 @@ public:
     void onReceived(const void* buffer, size_t size);
     //! Route this session's receive path through `batch` (nullptr: per call)
     void SetReceiveBatch(WSReceiveBatch* batch);
+    //! Route Send*Async through `batch`: frames are encoded at its next
+    //! Flush() (nullptr: encode per call).  Sync Send* flush it first, so the
+    //! connection's frames keep their order.
+    void SetSendBatch(WSSendBatch* batch);
     //! Transport closed (reference ws_session.cpp:20-38)
     void onDisconnected();
 
@@ -79,6 +83,7 @@ protected:
 
 private:
     WSReceiveBatch* _rx_batch{nullptr};
+    WSSendBatch* _tx_batch{nullptr};
     void ResetBuffers();
     size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0);
     bool SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status = 0);

@@ -138,6 +138,15 @@ int wsg_decode_batch_host(wsg_ctx* ctx, const uint8_t* wire, uint64_t wire_len,
                           const uint64_t* frame_start, uint32_t n,
                           uint8_t* out, wsg_recv_info* info);
 
+/* Batch encode of host buffers, synchronous, the bytes wsg_encode_batch
+ * produces: frames back to back in wire[0..wire_off[n]) (host pointers;
+ * wire_off[0..n] is filled).  Segments of ~32 MiB of frames flow through the
+ * same three stream slots; each segment's payloads are DMA'd as one range
+ * (or gathered through pinned staging when its descriptors are scattered).  */
+int wsg_encode_batch_host(wsg_ctx* ctx, const uint8_t* payload, uint64_t payload_len,
+                          const wsg_send_desc* desc, uint32_t n,
+                          uint8_t* wire, uint64_t wire_cap, uint64_t* wire_off);
+
 /* Page-locked host memory for receive/send buffers (DMA without staging). */
 int wsg_host_alloc(size_t bytes, void** out);
 int wsg_host_free(void* p);
@@ -201,6 +210,24 @@ int wsg_rx_forget(wsg_rx* rx, wsg_session* s);
 /* Complete frames and wire bytes queued for the next flush.                   */
 int wsg_rx_pending(wsg_rx* rx, uint32_t* frames, uint64_t* bytes);
 int wsg_rx_flush(wsg_rx* rx, wsg_rx_cb cb, void* user, uint32_t* delivered);
+
+/* ---- batched send over many sessions ------------- */
+/* wsg_tx_queue records PrepareSendFrame(opcode, mask, buf, size, status) for
+ * session s with its current send key (read under its send lock) and copies
+ * the payload; wsg_tx_flush encodes every queued frame in one pipelined GPU
+ * pass (wsg_encode_batch_host) and hands each frame to `sink` in queue order.
+ * The bytes are those wsg_session_prepare_send would produce.  One thread.  */
+typedef struct wsg_tx wsg_tx;
+typedef void (*wsg_tx_sink)(void* user, wsg_session* s, const uint8_t* frame,
+                            size_t size);
+int wsg_tx_create(wsg_ctx* ctx, wsg_tx** out);
+int wsg_tx_destroy(wsg_tx* tx);
+int wsg_tx_queue(wsg_tx* tx, wsg_session* s, uint8_t opcode, int mask,
+                 const void* buf, size_t size, int32_t status);
+/* Drop a session's queued frames (before wsg_session_destroy).                */
+int wsg_tx_forget(wsg_tx* tx, wsg_session* s);
+int wsg_tx_pending(wsg_tx* tx, uint32_t* frames, uint64_t* payload_bytes);
+int wsg_tx_flush(wsg_tx* tx, wsg_tx_sink sink, void* user, uint32_t* sent);
 
 /* ---- kernel timing (measurement hook used by bench.py) ------------------ */
 /* on = k > 0: the ctx records HIP events around the dominant payload kernel of

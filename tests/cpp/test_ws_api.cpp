@@ -3,6 +3,7 @@
 // tests/test_ws.cpp scenarios (echo :115-183, multicast byte totals
 // 4/8/12 :185-307, random soak :309-437) plus ping/pong and sync receive.
 // Payload masking runs on the GPU (needs a HIP device).
+#include "server/ws/ws_batch.h"
 #include "server/ws/ws_client.h"
 #include "server/ws/ws_server.h"
 #include "server/ws/ws_session.h"
@@ -325,6 +326,73 @@ static void test_batched_server_receive()
     CHECK(!server.IsBatchReceive());
 }
 
+// Batched send: clients share one send batch (masked
+// frames, one key per connection), the server batches its sessions' echoes;
+// nothing reaches a transport before the flush, and every connection's
+// frames keep their order (sync sends and multicasts flush first).
+static void test_batched_send()
+{
+    WSServer server;
+    std::vector<std::unique_ptr<Pair>> pairs;
+    for (int i = 0; i < 6; ++i) {
+        pairs.emplace_back(new Pair());
+        server.AddSession(pairs.back()->session);
+    }
+    server.EnableBatchSend(true);
+    CHECK(server.IsBatchSend());
+    WSSendBatch client_batch;
+    for (auto& p : pairs)
+        p->client->SetSendBatch(&client_batch);
+    std::mt19937 gen(5);
+    std::vector<std::vector<std::vector<uint8_t>>> sent(pairs.size());
+    for (int round = 0; round < 4; ++round) {
+        size_t frames = 0;
+        for (size_t i = 0; i < pairs.size(); ++i) {
+            const int k = 1 + int(gen() % 3);
+            for (int j = 0; j < k; ++j) {
+                std::vector<uint8_t> payload((gen() % 4 == 0) ? gen() % 70000 : gen() % 300);
+                for (auto& b : payload)
+                    b = uint8_t(gen());
+                CHECK(pairs[i]->client->SendBinaryAsync(payload.data(), payload.size()));
+                sent[i].push_back(payload);
+                ++frames;
+            }
+        }
+        bool quiet = true;
+        for (auto& p : pairs)
+            quiet = quiet && p->st.inbox.empty();
+        CHECK(quiet);
+        CHECK(client_batch.Flush() == frames);
+        for (auto& p : pairs)
+            p->pump();   // sessions receive and queue their echoes
+        for (auto& p : pairs)
+            quiet = quiet && p->ct.inbox.empty();
+        CHECK(quiet);
+        CHECK(server.FlushSend() == frames);
+        for (auto& p : pairs)
+            p->pump();
+    }
+    for (size_t i = 0; i < pairs.size(); ++i)
+        CHECK(pairs[i]->client->messages == sent[i]);
+
+    // order: an async frame queued before a sync send / a multicast goes first
+    auto& p = *pairs[0];
+    p.client->messages.clear();
+    p.session->SendTextAsync("a");
+    p.session->SendText("b");
+    server.MulticastText("c");
+    p.session->SendTextAsync("d");
+    CHECK(server.FlushSend() == 1);
+    p.pump();
+    std::vector<std::string> got;
+    for (auto& m : p.client->messages)
+        got.emplace_back(m.begin(), m.end());
+    CHECK(got == std::vector<std::string>({"a", "b", "c", "d"}));
+    for (auto& q : pairs)
+        q->client->SetSendBatch(nullptr);
+    server.EnableBatchSend(false);
+}
+
 int main()
 {
     try {
@@ -334,6 +402,7 @@ int main()
         test_sync_receive();
         test_soak();
         test_batched_server_receive();
+        test_batched_send();
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());
         return 2;
