@@ -68,6 +68,7 @@ def lib(path=None):
         "wsg_frame_size": (u64, [ctypes.c_uint8, ci, u64, i32]),
         "wsg_header_pack": (ci, [ctypes.c_uint8, ci, u64, i32, u32, vp]),
         "wsg_header_unpack": (ci, [vp, u64, vp]),
+        "wsg_ws_accept": (ci, [ctypes.c_char_p, sz, ctypes.c_char_p, sz]),
         "wsg_session_create": (ci, [vp, ctypes.POINTER(vp)]),
         "wsg_session_destroy": (ci, [vp]),
         "wsg_session_set_send_key": (ci, [vp, u32]),

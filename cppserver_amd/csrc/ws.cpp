@@ -7,8 +7,11 @@
 // the gfx950 kernel behind wsg_xor_host.  Reference semantics followed:
 // source/server/ws/ws.cpp:212-498, including the quirks of SURVEY.md §8a.
 #include "server/ws/ws.h"
+#include "server/ws/ws_handshake.h"
 #include "ws_session_impl.h"
 
+#include <algorithm>
+#include <cctype>
 #include <cstdlib>
 #include <cstring>
 #include <random>
@@ -33,6 +36,25 @@ void check(int rc, const char* what)
 {
     if (rc != WSG_OK)
         throw std::runtime_error(std::string(what) + ": " + wsg_strerror(rc));
+}
+
+bool iequal(std::string_view a, std::string_view b)
+{
+    if (a.size() != b.size())
+        return false;
+    for (size_t i = 0; i < a.size(); ++i)
+        if (std::tolower(static_cast<unsigned char>(a[i])) != std::tolower(static_cast<unsigned char>(b[i])))
+            return false;
+    return true;
+}
+
+std::string remove_blank(std::string_view s)
+{
+    std::string out;
+    for (char c : s)
+        if (!std::isspace(static_cast<unsigned char>(c)))
+            out.push_back(c);
+    return out;
 }
 
 uint32_t le32(const uint8_t k[4])
@@ -64,9 +86,119 @@ void WebSocket::set_send_key(uint32_t key) noexcept
 
 void WebSocket::InitWSNonce()
 {
-    thread_local std::mt19937 gen{std::random_device{}()};
+    // one rand() byte per nonce byte, as the reference (ws.cpp:21-24)
     for (auto& b : _ws_nonce)
-        b = uint8_t(gen());
+        b = uint8_t(std::rand());
+}
+
+bool WebSocket::PerformClientUpgrade(const HTTP::HTTPResponse& response)
+{
+    if (response.status() != 101)
+        return false;
+    bool error = false, accept = false, connection = false, upgrade = false;
+    for (size_t i = 0; i < response.headers(); ++i) {
+        const auto [key, value] = response.header(i);
+        if (iequal(key, "Connection")) {
+            if (!iequal(value, "Upgrade")) {
+                error = true;
+                onWSError("Invalid WebSocket handshaked response: 'Connection' header value must be 'Upgrade'");
+                break;
+            }
+            connection = true;
+        } else if (iequal(key, "Upgrade")) {
+            if (!iequal(value, "websocket")) {
+                error = true;
+                onWSError("Invalid WebSocket handshaked response: 'Upgrade' header value must be 'websocket'");
+                break;
+            }
+            upgrade = true;
+        } else if (iequal(key, "Sec-WebSocket-Accept")) {
+            const std::string expect = WSAcceptDigest(Base64Encode(ws_nonce()));
+            const std::string got = Base64Decode(value);
+            // compared as the reference does (ws.cpp:72-73): strncmp over the
+            // shorter length, so the bytes after a NUL in either are not compared
+            if (std::strncmp(got.c_str(), expect.c_str(), std::min(got.size(), expect.size())) != 0) {
+                error = true;
+                onWSError("Invalid WebSocket handshaked response: 'Sec-WebSocket-Accept' value validation failed");
+                break;
+            }
+            accept = true;
+        }
+    }
+    if (!accept || !connection || !upgrade) {
+        if (!error)
+            onWSError("Invalid WebSocket response");
+        return false;
+    }
+    Handshaked(true);
+    onWSConnected(response);
+    return true;
+}
+
+bool WebSocket::PerformServerUpgrade(const HTTP::HTTPRequest& request, HTTP::HTTPResponse& response)
+{
+    if (request.method() != "GET")
+        return false;
+    bool error = false, connection = false, upgrade = false, ws_key = false, ws_version = false;
+    std::string accept;
+    for (size_t i = 0; i < request.headers(); ++i) {
+        const auto [key, value] = request.header(i);
+        if (iequal(key, "Connection")) {
+            if (!iequal(value, "Upgrade") && !iequal(remove_blank(value), "keep-alive,Upgrade")) {
+                error = true;
+                response.MakeErrorResponse(400, "Invalid WebSocket handshaked request: 'Connection' header value "
+                                                "must be 'Upgrade' or 'keep-alive, Upgrade'");
+                break;
+            }
+            connection = true;
+        } else if (iequal(key, "Upgrade")) {
+            if (!iequal(value, "websocket")) {
+                error = true;
+                response.MakeErrorResponse(400, "Invalid WebSocket handshaked request: 'Upgrade' header value must "
+                                                "be 'websocket'");
+                break;
+            }
+            upgrade = true;
+        } else if (iequal(key, "Sec-WebSocket-Key")) {
+            if (value.empty()) {
+                error = true;
+                response.MakeErrorResponse(400, "Invalid WebSocket handshaked request: 'Sec-WebSocket-Key' header "
+                                                "value must be non empty");
+                break;
+            }
+            accept = WSAcceptKey(value);
+            ws_key = true;
+        } else if (iequal(key, "Sec-WebSocket-Version")) {
+            if (!iequal(value, "13")) {
+                error = true;
+                response.MakeErrorResponse(400, "Invalid WebSocket handshaked request: 'Sec-WebSocket-Version' "
+                                                "header value must be '13'");
+                break;
+            }
+            ws_version = true;
+        }
+    }
+    // not a WebSocket upgrade request at all: left to the HTTP layer
+    if (!connection && !upgrade && !ws_key && !ws_version)
+        return false;
+    if (!connection || !upgrade || !ws_key || !ws_version) {
+        if (!error)
+            response.MakeErrorResponse(400, "Invalid WebSocket response");
+        SendResponse(response);
+        return false;
+    }
+    response.Clear();
+    response.SetBegin(101, "HTTP/1.1");
+    response.SetHeader("Connection", "Upgrade");
+    response.SetHeader("Upgrade", "websocket");
+    response.SetHeader("Sec-WebSocket-Accept", accept);
+    response.SetBody();
+    if (!onWSConnecting(request, response))
+        return false;
+    SendResponse(response);
+    Handshaked(false);
+    onWSConnected(request);
+    return true;
 }
 
 void WebSocket::Handshaked(bool client)

@@ -66,10 +66,12 @@ bool WSClient::Connect()
     if (!_transport.IsConnected())
         return false;
     ResetBuffers();
-    InitWSNonce();
-    Handshaked(true);
-    onWSConnected();
-    return true;
+    _http_buf.clear();
+    HTTP::HTTPRequest request;
+    onWSConnecting(request);
+    request.SetBody();
+    const std::string& req = request.cache();
+    return _transport.Send(req.data(), req.size()) == req.size();
 }
 
 bool WSClient::Disconnect()
@@ -91,8 +93,29 @@ void WSClient::onDisconnected()
 
 void WSClient::onReceived(const void* buffer, size_t size)
 {
-    if (!_ws_handshaked)
+    if (!_ws_handshaked) {
+        // the upgrade response (reference ws_client.cpp:76-116 via HTTPClient)
+        _http_buf.append(static_cast<const char*>(buffer), size);
+        HTTP::HTTPResponse response;
+        const size_t used = response.Parse(_http_buf);
+        if (used == 0)
+            return;   // header block not complete yet
+        const std::string rest = _http_buf.substr(used);
+        _http_buf.clear();
+        if (response.error()) {
+            onWSError("Invalid HTTP response");
+            return;
+        }
+        if (!PerformClientUpgrade(response) || rest.empty())
+            return;
+        buffer = rest.data();   // frames that came with the response
+        size = rest.size();
+        if (_rx_batch)
+            _rx_batch->Feed(*this, buffer, size);
+        else
+            PrepareReceiveFrame(buffer, size);
         return;
+    }
     if (_rx_batch)
         _rx_batch->Feed(*this, buffer, size);
     else
@@ -175,8 +198,7 @@ bool WSSession::Connect()
     if (!_transport.IsConnected())
         return false;
     ResetBuffers();
-    Handshaked(false);
-    onWSConnected();
+    _http_buf.clear();
     return true;
 }
 
@@ -199,8 +221,29 @@ void WSSession::onDisconnected()
 
 void WSSession::onReceived(const void* buffer, size_t size)
 {
-    if (!_ws_handshaked)
+    if (!_ws_handshaked) {
+        // the upgrade request (reference ws_session.cpp:53-65 via HTTPSession)
+        _http_buf.append(static_cast<const char*>(buffer), size);
+        HTTP::HTTPRequest request;
+        const size_t used = request.Parse(_http_buf);
+        if (used == 0)
+            return;
+        const std::string rest = _http_buf.substr(used);
+        _http_buf.clear();
+        HTTP::HTTPResponse response;
+        if (request.error()) {
+            response.MakeErrorResponse(400, "Invalid HTTP request");
+            SendResponse(response);
+            return;
+        }
+        if (!PerformServerUpgrade(request, response) || rest.empty())
+            return;
+        if (_rx_batch)
+            _rx_batch->Feed(*this, rest.data(), rest.size());
+        else
+            PrepareReceiveFrame(rest.data(), rest.size());
         return;
+    }
     if (_rx_batch)
         _rx_batch->Feed(*this, buffer, size);
     else

@@ -9,14 +9,18 @@
  * header state machine stays on the host thread that owns the connection,
  * as it does in the reference.
  *
- * Not carried over (handshake): PerformClientUpgrade,
- * PerformServerUpgrade and the HTTP-typed onWSConnecting/onWSConnected
- * overloads; Handshaked() below stands in for a completed upgrade.
+ * The upgrade handshake is here too:
+ * PerformClientUpgrade / PerformServerUpgrade over the HTTP request/response
+ * subset of include/server/http/, with the reference's onWSConnecting /
+ * onWSConnected hooks.  The reference's client variant also takes the
+ * connection's UUID, which it does not use; it is dropped here.
  */
 #ifndef CPPSERVER_AMD_WS_H
 #define CPPSERVER_AMD_WS_H
 
 #include "wsg_capi.h"
+#include "server/http/http_request.h"
+#include "server/http/http_response.h"
 
 #include <array>
 #include <cstddef>
@@ -70,6 +74,17 @@ public:
     //! Initialize WebSocket random nonce
     void InitWSNonce();
 
+    //! Validate the server's upgrade response (reference ws.cpp:26-101):
+    //! status 101, Connection: Upgrade, Upgrade: websocket and the
+    //! Sec-WebSocket-Accept digest of this connection's nonce.  On success
+    //! the connection is handshaked with a random send key, onWSConnected(response).
+    bool PerformClientUpgrade(const HTTP::HTTPResponse& response);
+    //! Answer a client's upgrade request (reference ws.cpp:103-210): validate
+    //! it, build the 101 response (or a 400 error), let onWSConnecting veto
+    //! it, SendResponse(), handshake with send key 0, onWSConnected(request).
+    //! Returns false for a request that is not a WebSocket upgrade at all.
+    bool PerformServerUpgrade(const HTTP::HTTPRequest& request, HTTP::HTTPResponse& response);
+
     //! Mark the upgrade as done and install the send key: a client draws a
     //! random key per connection (reference ws.cpp:97), a server session
     //! uses 0 (ws.cpp:206).
@@ -83,13 +98,23 @@ protected:
     //! Codec context of this connection (the explicit one, else ThreadCodec())
     wsg_ctx* codec();
 
-    virtual void onWSConnected() {}
+    //! Client: fill the upgrade request (reference ws.h:107)
+    virtual void onWSConnecting(HTTP::HTTPRequest& request) {}
+    //! Client: upgrade accepted (reference ws.h:112)
+    virtual void onWSConnected(const HTTP::HTTPResponse& response) {}
+    //! Server: veto or amend the upgrade response (reference ws.h:124)
+    virtual bool onWSConnecting(const HTTP::HTTPRequest& request, HTTP::HTTPResponse& response) { return true; }
+    //! Server: upgrade done (reference ws.h:129)
+    virtual void onWSConnected(const HTTP::HTTPRequest& request) {}
     virtual void onWSDisconnected() {}
     virtual void onWSReceived(const void* buffer, size_t size) {}
     virtual void onWSClose(const void* buffer, size_t size, int status = 1000) {}
     virtual void onWSPing(const void* buffer, size_t size) {}
     virtual void onWSPong(const void* buffer, size_t size) {}
     virtual void onWSError(const std::string& message) {}
+
+    //! Send the upgrade response (reference ws.h:202; sessions override it)
+    virtual void SendResponse(const HTTP::HTTPResponse& response) {}
 
 protected:
     // Per-connection codec state, named as in the reference so that

@@ -23,7 +23,10 @@ public:
     explicit WSClient(Transport& transport, wsg_ctx* codec = nullptr) : WebSocket(codec), _transport(transport) {}
     virtual ~WSClient() = default;
 
-    //! Complete the connection: clear buffers, upgrade (random client key), onWSConnected
+    //! Start the upgrade on a connected transport (reference WSClient::onConnected,
+    //! ws_client.cpp:38-53): clear buffers, let onWSConnecting fill the
+    //! request, send it.  The connection is handshaked when the server's 101
+    //! response arrives through onReceived (PerformClientUpgrade).
     virtual bool Connect();
     virtual bool Disconnect();
     bool IsConnected() const { return _transport.IsConnected() && _ws_handshaked; }
@@ -87,6 +90,7 @@ protected:
     Transport& _transport;
 
 private:
+    std::string _http_buf;   // upgrade response bytes until its header block is complete
     WSReceiveBatch* _rx_batch{nullptr};
     WSSendBatch* _tx_batch{nullptr};
     void ResetBuffers();

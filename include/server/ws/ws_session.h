@@ -24,7 +24,9 @@ public:
     explicit WSSession(Transport& transport, wsg_ctx* codec = nullptr) : WebSocket(codec), _transport(transport) {}
     virtual ~WSSession() = default;
 
-    //! Upgrade accepted: clear buffers, key 0, onWSConnected
+    //! Accept a connected transport: clear buffers and wait for the client's
+    //! upgrade request, answered through onReceived (PerformServerUpgrade,
+    //! reference ws_session.cpp:53-65)
     virtual bool Connect();
     virtual bool Disconnect();
     bool IsConnected() const { return _transport.IsConnected() && _ws_handshaked; }
@@ -78,10 +80,16 @@ public:
 protected:
     void onWSClose(const void* buffer, size_t size, int status = 1000) override { Close(); }
     void onWSPing(const void* buffer, size_t size) override { SendPongAsync(buffer, size); }
+    //! The upgrade response goes out on the transport (reference ws_session.h:107)
+    void SendResponse(const HTTP::HTTPResponse& response) override
+    {
+        _transport.SendAsync(response.cache().data(), response.cache().size());
+    }
 
     Transport& _transport;
 
 private:
+    std::string _http_buf;   // upgrade request bytes until its header block is complete
     WSReceiveBatch* _rx_batch{nullptr};
     WSSendBatch* _tx_batch{nullptr};
     void ResetBuffers();

@@ -161,6 +161,11 @@ int wsg_header_pack(uint8_t opcode, int mask, uint64_t len, int32_t status,
  * or WSG_ETRUNC when avail is too short for the header.                       */
 int wsg_header_unpack(const uint8_t* buf, uint64_t avail, wsg_recv_info* info);
 
+/* ---- upgrade handshake (host; reference ws.cpp:26-210) ------------------ */
+/* Sec-WebSocket-Accept for a Sec-WebSocket-Key: Base64(SHA-1(key + RFC 6455
+ * GUID)), NUL-terminated in out[0..29).                                       */
+int wsg_ws_accept(const char* key, size_t key_len, char* out, size_t out_cap);
+
 /* ---- per-connection session (the WebSocket mix-in, ws.h:29) ------------- */
 /* A session is the reference's per-connection codec state; its payload
  * mask/unmask runs on the GPU through the owning ctx.                         */

@@ -1,0 +1,233 @@
+// test_handshake.cpp — the WebSocket upgrade (reference ws.cpp:26-210) and
+// its HTTP subset, host only (no frame is sent, so no GPU is needed):
+// RFC 6455 / RFC 4648 known answers, request/response round trips, the
+// reference's accept/reject rules and error texts, and a full client/session
+// upgrade over an in-memory transport.
+#include "server/http/http_request.h"
+#include "server/http/http_response.h"
+#include "server/ws/ws_client.h"
+#include "server/ws/ws_handshake.h"
+#include "server/ws/ws_session.h"
+
+#include <cstdio>
+#include <deque>
+#include <string>
+#include <vector>
+
+using namespace CppServer;
+using namespace CppServer::WS;
+
+static int g_failures = 0, g_checks = 0;
+#define CHECK(cond)                                                                    \
+    do {                                                                               \
+        ++g_checks;                                                                    \
+        if (!(cond)) {                                                                 \
+            ++g_failures;                                                              \
+            std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+        }                                                                              \
+    } while (0)
+
+static void test_known_answers()
+{
+    // RFC 6455 §1.3 worked example
+    CHECK(WSAcceptKey("dGhlIHNhbXBsZSBub25jZQ==") == "s3pPLMBiTxaQ9kYGzzhZRbK+xOo=");
+    // RFC 4648 §10 test vectors
+    const char* plain[] = {"", "f", "fo", "foo", "foob", "fooba", "foobar"};
+    const char* coded[] = {"", "Zg==", "Zm8=", "Zm9v", "Zm9vYg==", "Zm9vYmE=", "Zm9vYmFy"};
+    for (int i = 0; i < 7; ++i) {
+        CHECK(Base64Encode(plain[i]) == coded[i]);
+        CHECK(Base64Decode(coded[i]) == plain[i]);
+    }
+    char out[29];
+    CHECK(wsg_ws_accept("dGhlIHNhbXBsZSBub25jZQ==", 24, out, sizeof(out)) == WSG_OK);
+    CHECK(std::string(out) == "s3pPLMBiTxaQ9kYGzzhZRbK+xOo=");
+    CHECK(wsg_ws_accept("x", 1, out, 10) == WSG_ENOMEM);
+}
+
+static void test_http_round_trip()
+{
+    HTTP::HTTPRequest rq("GET", "/chat");
+    rq.SetHeader("Host", "localhost").SetHeader("Upgrade", "websocket").SetBody("xy");
+    CHECK(rq.cache() == "GET /chat HTTP/1.1\r\nHost: localhost\r\nUpgrade: websocket\r\nContent-Length: 2\r\n\r\nxy");
+    HTTP::HTTPRequest back;
+    const std::string wire = rq.cache() + "trailing";
+    CHECK(back.Parse(wire) == rq.cache().size());
+    CHECK(!back.error() && back.method() == "GET" && back.url() == "/chat" && back.protocol() == "HTTP/1.1");
+    CHECK(back.headers() == 3 && std::get<1>(back.header(1)) == "websocket" && back.body() == "xy");
+    CHECK(back.Parse(rq.cache().substr(0, 20)) == 0);   // incomplete
+    HTTP::HTTPResponse rs;
+    rs.MakeErrorResponse(400, "bad");
+    CHECK(rs.cache() == "HTTP/1.1 400 Bad Request\r\nContent-Type: text/plain; charset=UTF-8\r\nContent-Length: 3\r\n\r\nbad");
+    HTTP::HTTPResponse rb;
+    CHECK(rb.Parse(rs.cache()) == rs.cache().size() && rb.status() == 400 && rb.status_phrase() == "Bad Request");
+    CHECK(rb.body() == "bad");
+    HTTP::HTTPResponse junk;
+    junk.Parse("HTTP/1.1 abc Nope\r\n\r\n");
+    CHECK(junk.error());
+}
+
+struct Server : WebSocket {
+    std::vector<std::string> sent;
+    bool connected = false;
+    bool veto = false;
+    void SendResponse(const HTTP::HTTPResponse& r) override { sent.push_back(r.cache()); }
+    bool onWSConnecting(const HTTP::HTTPRequest&, HTTP::HTTPResponse&) override { return !veto; }
+    void onWSConnected(const HTTP::HTTPRequest&) override { connected = true; }
+    using WebSocket::_ws_handshaked;
+};
+
+struct Client : WebSocket {
+    std::vector<std::string> errors;
+    bool connected = false;
+    void onWSError(const std::string& m) override { errors.push_back(m); }
+    void onWSConnected(const HTTP::HTTPResponse&) override { connected = true; }
+    using WebSocket::_ws_handshaked;
+};
+
+static HTTP::HTTPRequest upgrade_request(std::string_view key, std::string_view version = "13",
+                                         std::string_view connection = "Upgrade")
+{
+    HTTP::HTTPRequest r("GET", "/");
+    r.SetHeader("Host", "localhost").SetHeader("Upgrade", "websocket").SetHeader("Connection", connection);
+    r.SetHeader("Sec-WebSocket-Key", key).SetHeader("Sec-WebSocket-Version", version).SetBody();
+    return r;
+}
+
+static void test_server_rules()
+{
+    Client c;
+    const std::string key = Base64Encode(c.ws_nonce());
+    {
+        Server s;
+        HTTP::HTTPResponse resp;
+        CHECK(s.PerformServerUpgrade(upgrade_request(key), resp));
+        CHECK(s.connected && s._ws_handshaked && s.send_key() == 0);   // server key 0 (ws.cpp:206)
+        CHECK(s.sent.size() == 1 && resp.status() == 101);
+        CHECK(s.sent[0] == "HTTP/1.1 101 Switching Protocols\r\nConnection: Upgrade\r\nUpgrade: websocket\r\n"
+                           "Sec-WebSocket-Accept: " + WSAcceptKey(key) + "\r\nContent-Length: 0\r\n\r\n");
+        // the client accepts that response (random key, ws.cpp:97)
+        HTTP::HTTPResponse back;
+        back.Parse(s.sent[0]);
+        CHECK(c.PerformClientUpgrade(back) && c.connected && c._ws_handshaked && c.errors.empty());
+    }
+    {
+        Server s;   // "keep-alive, Upgrade" is accepted too (ws.cpp:123)
+        HTTP::HTTPResponse resp;
+        CHECK(s.PerformServerUpgrade(upgrade_request(key, "13", "keep-alive, Upgrade"), resp));
+    }
+    {
+        Server s;   // wrong version: 400 with the reference's text, sent
+        HTTP::HTTPResponse resp;
+        CHECK(!s.PerformServerUpgrade(upgrade_request(key, "12"), resp));
+        CHECK(resp.status() == 400 && s.sent.size() == 1 && !s._ws_handshaked);
+        CHECK(resp.body() == "Invalid WebSocket handshaked request: 'Sec-WebSocket-Version' header value must be '13'");
+    }
+    {
+        Server s;   // not an upgrade at all: left alone, nothing sent
+        HTTP::HTTPRequest plain("GET", "/index.html");
+        plain.SetHeader("Host", "x").SetBody();
+        HTTP::HTTPResponse resp;
+        CHECK(!s.PerformServerUpgrade(plain, resp) && s.sent.empty());
+        HTTP::HTTPRequest post("POST", "/");
+        post.SetBody();
+        CHECK(!s.PerformServerUpgrade(post, resp) && s.sent.empty());
+    }
+    {
+        Server s;   // onWSConnecting veto: no response, not handshaked
+        s.veto = true;
+        HTTP::HTTPResponse resp;
+        CHECK(!s.PerformServerUpgrade(upgrade_request(key), resp) && s.sent.empty() && !s._ws_handshaked);
+    }
+}
+
+static void test_client_rules()
+{
+    Client c;
+    HTTP::HTTPResponse r(101);
+    r.SetHeader("Connection", "Upgrade").SetHeader("Upgrade", "websocket");
+    r.SetHeader("Sec-WebSocket-Accept", WSAcceptKey("some other key")).SetBody();
+    CHECK(!c.PerformClientUpgrade(r) && !c._ws_handshaked);
+    CHECK(c.errors.size() == 1 &&
+          c.errors[0] == "Invalid WebSocket handshaked response: 'Sec-WebSocket-Accept' value validation failed");
+    HTTP::HTTPResponse missing(101);
+    missing.SetHeader("Connection", "Upgrade").SetBody();
+    CHECK(!c.PerformClientUpgrade(missing) && c.errors.back() == "Invalid WebSocket response");
+    HTTP::HTTPResponse not101(200);
+    not101.SetBody();
+    const size_t errs = c.errors.size();
+    CHECK(!c.PerformClientUpgrade(not101) && c.errors.size() == errs);   // silently not an upgrade
+}
+
+// in-memory transport pair
+struct Loop : Transport {
+    Loop* peer = nullptr;
+    std::deque<uint8_t> inbox;
+    size_t Send(const void* b, size_t n) override
+    {
+        const uint8_t* p = static_cast<const uint8_t*>(b);
+        peer->inbox.insert(peer->inbox.end(), p, p + n);
+        return n;
+    }
+    bool SendAsync(const void* b, size_t n) override { return Send(b, n) == n; }
+    size_t Receive(void*, size_t) override { return 0; }
+    bool Disconnect() override { return true; }
+    bool IsConnected() const override { return true; }
+};
+
+struct MyClient : WSClient {
+    using WSClient::WSClient;
+    bool up = false;
+    void onWSConnecting(HTTP::HTTPRequest& request) override
+    {
+        request.SetBegin("GET", "/");
+        request.SetHeader("Host", "localhost");
+        request.SetHeader("Upgrade", "websocket");
+        request.SetHeader("Connection", "Upgrade");
+        request.SetHeader("Sec-WebSocket-Key", Base64Encode(ws_nonce()));
+        request.SetHeader("Sec-WebSocket-Version", "13");
+    }
+    void onWSConnected(const HTTP::HTTPResponse&) override { up = true; }
+};
+
+struct MySession : WSSession {
+    using WSSession::WSSession;
+    bool up = false;
+    void onWSConnected(const HTTP::HTTPRequest&) override { up = true; }
+};
+
+static void test_client_session_upgrade()
+{
+    Loop a, b;
+    a.peer = &b;
+    b.peer = &a;
+    MyClient client(a);
+    MySession session(b);
+    CHECK(session.Connect() && !session.IsConnected());
+    CHECK(client.Connect() && !client.IsConnected());
+    // deliver the request to the session one byte at a time, the response whole
+    std::vector<uint8_t> req(b.inbox.begin(), b.inbox.end());
+    b.inbox.clear();
+    for (uint8_t byte : req)
+        session.onReceived(&byte, 1);
+    CHECK(session.up && session.IsConnected());
+    std::vector<uint8_t> resp(a.inbox.begin(), a.inbox.end());
+    a.inbox.clear();
+    client.onReceived(resp.data(), resp.size());
+    CHECK(client.up && client.IsConnected());
+}
+
+int main()
+{
+    try {
+        test_known_answers();
+        test_http_round_trip();
+        test_server_rules();
+        test_client_rules();
+        test_client_session_upgrade();
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "exception: %s\n", e.what());
+        return 2;
+    }
+    std::printf("%d checks, %d failures\n", g_checks, g_failures);
+    return g_failures == 0 ? 0 : 1;
+}

@@ -5,6 +5,7 @@
 // Payload masking runs on the GPU (needs a HIP device).
 #include "server/ws/ws_batch.h"
 #include "server/ws/ws_client.h"
+#include "server/ws/ws_handshake.h"
 #include "server/ws/ws_server.h"
 #include "server/ws/ws_session.h"
 
@@ -67,7 +68,19 @@ struct EchoClient : WSClient {
     size_t received = 0;
     std::vector<std::vector<uint8_t>> messages, pongs;
     bool connected = false, disconnected = false;
-    void onWSConnected() override { connected = true; }
+    // the upgrade request, as the reference's ws_chat_client example fills it
+    void onWSConnecting(CppServer::HTTP::HTTPRequest& request) override
+    {
+        request.SetBegin("GET", "/");
+        request.SetHeader("Host", "localhost");
+        request.SetHeader("Origin", "http://localhost");
+        request.SetHeader("Upgrade", "websocket");
+        request.SetHeader("Connection", "Upgrade");
+        request.SetHeader("Sec-WebSocket-Key", Base64Encode(ws_nonce()));
+        request.SetHeader("Sec-WebSocket-Protocol", "chat, superchat");
+        request.SetHeader("Sec-WebSocket-Version", "13");
+    }
+    void onWSConnected(const CppServer::HTTP::HTTPResponse& response) override { connected = true; }
     void onWSDisconnected() override { disconnected = true; }
     void onWSReceived(const void* b, size_t n) override
     {
@@ -110,6 +123,7 @@ struct Pair {
         session = std::make_shared<EchoSession>(st);
         session->Connect();
         client->Connect();
+        pump();   // upgrade request -> 101 response
     }
     // deliver queued bytes until both inboxes are empty
     void pump()

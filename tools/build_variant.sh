@@ -14,5 +14,6 @@ $H $F -c $root/cppserver_amd/csrc/wsg_capi.hip -o c.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws.cpp -o w.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws_api.cpp -o a.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws_batch.cpp -o b.o
-$H --offload-arch=gfx950 -shared -o libwsg.so k.o c.o w.o a.o b.o
+$H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/http.cpp -o h.o
+$H --offload-arch=gfx950 -shared -o libwsg.so k.o c.o w.o a.o b.o h.o -lcrypto
 echo "$out/libwsg.so"

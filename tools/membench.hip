@@ -71,6 +71,67 @@ __global__ __launch_bounds__(BLOCK) void k_wavepiece(const u32x4* __restrict__ s
     }
 }
 
+// Tile -> block mappings for a streaming copy-with-XOR (16 KiB tiles):
+//  MAP 0: grid-stride (tile t to block t % grid)
+//  MAP 1: XCD-partitioned: blocks are dealt to the 8 XCDs round-robin
+//         (block b runs on XCD b % 8), so XCD x streams the x-th eighth of
+//         the buffer, grid-stride within it
+//  MAP 2: block-contiguous runs (block b streams tiles [b*T/grid, (b+1)*T/grid))
+template <int MAP>
+__global__ __launch_bounds__(256) void k_map(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n16,
+                                             uint32_t key)
+{
+    constexpr int U = 4;
+    const uint64_t per_tile = 256ull * U;
+    const uint64_t tiles = n16 / per_tile;
+    uint64_t t0, t1, stride;
+    if (MAP == 0) {
+        t0 = blockIdx.x;
+        t1 = tiles;
+        stride = gridDim.x;
+    } else if (MAP == 1) {
+        const uint64_t x = blockIdx.x % 8, per = gridDim.x / 8;
+        t0 = x * tiles / 8 + blockIdx.x / 8;
+        t1 = (x + 1) * tiles / 8;
+        stride = per;
+    } else {
+        t0 = uint64_t(blockIdx.x) * tiles / gridDim.x;
+        t1 = uint64_t(blockIdx.x + 1) * tiles / gridDim.x;
+        stride = 1;
+    }
+    for (uint64_t t = t0; t < t1; t += stride) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            v[u] = __builtin_nontemporal_load(src + t * per_tile + uint64_t(u) * 256 + threadIdx.x);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_nontemporal_store(v[u] ^ key, dst + t * per_tile + uint64_t(u) * 256 + threadIdx.x);
+    }
+}
+
+template <int MAP>
+void run_map(const char* name, u32x4* const* srcs, u32x4* const* dsts, uint64_t n16, int grid)
+{
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 4; ++i)
+        k_map<MAP><<<grid, 256>>>(srcs[i & 1], dsts[i & 1], n16, 7u);
+    const int reps = 40;
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i)
+        k_map<MAP><<<grid, 256>>>(srcs[i & 1], dsts[i & 1], n16, 7u);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    ms /= reps;
+    printf("%-28s grid=%6d  %8.1f us  %7.1f GB/s\n", name, grid, ms * 1e3, 2.0 * n16 * 16 / (ms * 1e-3) / 1e9);
+    CK(hipEventDestroy(a));
+    CK(hipEventDestroy(b));
+}
+
 // Write-only stream (the fan-out's shape): every lane stores U chunks.
 template <int BLOCK, int U, int NT>
 __global__ __launch_bounds__(BLOCK) void k_fill(u32x4* __restrict__ dst, uint64_t n16, uint32_t key)
@@ -189,6 +250,28 @@ int main(int argc, char** argv)
             run_wp<256, 8>("wave-piece 8K", src, dst, n16, cus, 16);
             run_wp<256, 16>("wave-piece 16K", src, dst, n16, cus, 8);
         }
+        CK(hipFree(src));
+        CK(hipFree(dst));
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "map") {
+        // C2-sized copy (argv[1] MiB per buffer), two buffer pairs alternating
+        // so that no launch re-reads what the previous one left in the MALL
+        u32x4 *s2, *d2;
+        CK(hipMalloc(&s2, bytes));
+        CK(hipMalloc(&d2, bytes));
+        CK(hipMemset(s2, 2, bytes));
+        u32x4* srcs[2] = {src, s2};
+        u32x4* dsts[2] = {dst, d2};
+        for (int rep = 0; rep < 2; ++rep)
+            for (int bpc : {8, 16, 32}) {
+                const int grid = cus * bpc;
+                run_map<0>("grid-stride", srcs, dsts, n16, grid);
+                run_map<1>("xcd-partitioned", srcs, dsts, n16, grid);
+                run_map<2>("block-contiguous", srcs, dsts, n16, grid);
+            }
+        CK(hipFree(s2));
+        CK(hipFree(d2));
         CK(hipFree(src));
         CK(hipFree(dst));
         return 0;
