@@ -148,7 +148,7 @@ class Workload:
             self.wire = torch.empty(fsz * k, dtype=torch.uint8, device=device)
             self.payload_bytes = length * k
             self.alg_bytes = fsz * k + length + 4 * k
-            self.kernel = "k_fanout"
+            self.kernel = "k_fanout_flat"
             self.workload = "C4 fan-out: one %d B payload masked with %d client keys" % (length, k)
             self.extra = {"keys": k, "wire_bytes": fsz * k}
         else:  # c5: this rank's round-robin shard of 1 Mi x 16 KiB frames, encode
@@ -269,6 +269,21 @@ def pcie_inclusive(w, reps=3):
         for _ in range(reps):
             w.codec.decode_batch_host(src, fs, out=dst)
         res[name] = round(w.payload_bytes / ((time.perf_counter() - t0) / reps) / GIB, 2)
+    # the send direction: the same 4096 x 64 KiB payloads encoded from host
+    # memory (wsg_encode_batch_host), pinned buffers
+    from cppserver_amd import workloads as wl
+
+    rng = np.random.default_rng(7)
+    desc, total = wl.ragged_desc(rng, np.full(len(fs), w.payload_bytes // len(fs)))
+    pay = ca.pinned_empty(total)
+    pay[:] = wl.random_bytes(rng, total)
+    out = ca.pinned_empty(int(ca.frame_sizes(desc).sum()))
+    rc, _, _ = w.codec.encode_batch_host(pay, desc, wire=out)
+    assert rc == 0
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        w.codec.encode_batch_host(pay, desc, wire=out)
+    res["encode_pinned"] = round(total / ((time.perf_counter() - t0) / reps) / GIB, 2)
     return res
 
 

@@ -15,7 +15,7 @@ import numpy as np
 
 from .layout import (  # noqa: F401  (re-exported)
     CB_CLOSE, CB_PING, CB_PONG, CB_RECEIVED, RECV_INFO, SEND_DESC, WS_BINARY, WS_CLOSE, WS_FIN, WS_PING,
-    WS_PONG, WS_TEXT, WSG_EHIP, WSG_EINVAL, WSG_ENOMEM, WSG_ETRUNC, WSG_OK, frame_size, key_from_bytes,
+    WS_PONG, WS_TEXT, WSG_EHIP, WSG_EINVAL, WSG_ENOMEM, WSG_ETRUNC, WSG_OK, frame_size, frame_sizes, key_from_bytes,
 )
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -260,7 +260,7 @@ class Codec:
         payload = np.ascontiguousarray(payload, dtype=np.uint8)
         desc = np.ascontiguousarray(desc, dtype=SEND_DESC)
         n = len(desc)
-        total = int(sum(frame_size(int(d["opcode"]), bool(d["mask"]), int(d["len"]), int(d["status"])) for d in desc))
+        total = int(frame_sizes(desc).sum()) if n else 0
         if wire is None:
             wire = np.empty(max(total, 1), dtype=np.uint8)
         off = np.zeros(n + 1, dtype=np.uint64)

@@ -41,7 +41,9 @@ struct wsg_ctx {
     // pipelined host path (wsg_decode_batch_host): one stream + staging per slot
     struct Slot {
         hipStream_t stream = nullptr;
-        hipEvent_t done = nullptr;
+        hipEvent_t done = nullptr;       // the segment's last copy back has finished
+        hipEvent_t h2d_done = nullptr;   // role pipeline: inputs are in HBM
+        hipEvent_t k_done = nullptr;     // role pipeline: kernels have finished
         uint8_t* d_wire = nullptr;       // segment, decoded in place
         uint64_t wire_cap = 0;
         uint8_t* h_in = nullptr;         // pinned staging for pageable callers
@@ -74,6 +76,11 @@ struct wsg_ctx {
     };
     static constexpr int kSlots = 3;
     Slot slots[kSlots];
+    // role streams of the host pipelines: every H2D copy on one stream, every
+    // kernel on another, every D2H copy on a third, so the two copy directions
+    // run concurrently while kernels run between them ($WSG_PIPE=slots: one
+    // stream per slot instead, the earlier design, kept for A/B runs)
+    hipStream_t s_h2d = nullptr, s_kern = nullptr, s_d2h = nullptr;
     // timing of the dominant kernel
     struct EvPair {
         hipEvent_t a, b;
@@ -300,6 +307,11 @@ int wsg_destroy(wsg_ctx* c)
     (void)hipFree(c->d_info);
     if (c->h_stage)
         (void)hipHostFree(c->h_stage);
+    for (hipStream_t r : {c->s_h2d, c->s_kern, c->s_d2h})
+        if (r) {
+            (void)hipStreamSynchronize(r);
+            (void)hipStreamDestroy(r);
+        }
     for (auto& sl : c->slots) {
         if (sl.stream)
             (void)hipStreamSynchronize(sl.stream);
@@ -323,6 +335,10 @@ int wsg_destroy(wsg_ctx* c)
             (void)hipHostFree(sl.h_info);
         if (sl.done)
             (void)hipEventDestroy(sl.done);
+        if (sl.h2d_done)
+            (void)hipEventDestroy(sl.h2d_done);
+        if (sl.k_done)
+            (void)hipEventDestroy(sl.k_done);
         if (sl.stream)
             (void)hipStreamDestroy(sl.stream);
     }
@@ -487,12 +503,63 @@ bool host_pinned(const void* p)
     return a.type == hipMemoryTypeHost;
 }
 
+int slot_init(wsg_ctx::Slot& sl)
+{
+    if (sl.stream)
+        return WSG_OK;
+    WSG_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+    WSG_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    WSG_HIP(hipEventCreateWithFlags(&sl.h2d_done, hipEventDisableTiming));
+    WSG_HIP(hipEventCreateWithFlags(&sl.k_done, hipEventDisableTiming));
+    return WSG_OK;
+}
+
+// The three streams one segment's work goes to, and the hand-offs between
+// them: H2D copies, then kernels, then D2H copies.
+struct Pipe {
+    hipStream_t h2d, kern, d2h;
+    bool roles;
+};
+
+int pipe_for(wsg_ctx* c, wsg_ctx::Slot& sl, Pipe& p)
+{
+    const char* e = std::getenv("WSG_PIPE");
+    p.roles = !(e && std::strcmp(e, "slots") == 0);
+    if (!p.roles) {
+        p.h2d = p.kern = p.d2h = sl.stream;
+        return WSG_OK;
+    }
+    for (hipStream_t* r : {&c->s_h2d, &c->s_kern, &c->s_d2h})
+        if (!*r)
+            WSG_HIP(hipStreamCreateWithFlags(r, hipStreamNonBlocking));
+    p.h2d = c->s_h2d;
+    p.kern = c->s_kern;
+    p.d2h = c->s_d2h;
+    return WSG_OK;
+}
+
+// inputs copied -> kernels may start; kernels done -> copies back may start
+int pipe_to_kern(const Pipe& p, wsg_ctx::Slot& sl)
+{
+    if (p.roles) {
+        WSG_HIP(hipEventRecord(sl.h2d_done, p.h2d));
+        WSG_HIP(hipStreamWaitEvent(p.kern, sl.h2d_done, 0));
+    }
+    return WSG_OK;
+}
+int pipe_to_d2h(const Pipe& p, wsg_ctx::Slot& sl)
+{
+    if (p.roles) {
+        WSG_HIP(hipEventRecord(sl.k_done, p.kern));
+        WSG_HIP(hipStreamWaitEvent(p.d2h, sl.k_done, 0));
+    }
+    return WSG_OK;
+}
+
 int slot_reserve(wsg_ctx::Slot& sl, uint64_t bytes, uint64_t frames, bool need_host)
 {
-    if (!sl.stream) {
-        WSG_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
-        WSG_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
-    }
+    if (int rc = slot_init(sl))
+        return rc;
     if (int rc = ensure_array(sl.d_wire, sl.wire_cap, bytes + 32))
         return rc;
     if (int rc = ensure_array(sl.d_tiles, sl.tiles_cap, ceil_div(bytes + 32, wsg::TILE)))
@@ -625,26 +692,33 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
             std::memcpy(sl.h_in, wire + base, len);
             src = sl.h_in;
         }
-        WSG_HIP(hipMemcpyAsync(sl.d_wire, src, len, hipMemcpyHostToDevice, sl.stream));
-        WSG_HIP(hipMemcpyAsync(sl.d_fs, sl.h_fs, m * sizeof(uint64_t), hipMemcpyHostToDevice, sl.stream));
-        if (int rc = decode_launch(c, sl.d_wire, len, sl.d_fs, m, sl.d_wire, sl.d_info, sl.d_tiles, sl.stream))
+        Pipe pp;
+        if (int rc = pipe_for(c, sl, pp))
+            return rc;
+        WSG_HIP(hipMemcpyAsync(sl.d_wire, src, len, hipMemcpyHostToDevice, pp.h2d));
+        WSG_HIP(hipMemcpyAsync(sl.d_fs, sl.h_fs, m * sizeof(uint64_t), hipMemcpyHostToDevice, pp.h2d));
+        if (int rc = pipe_to_kern(pp, sl))
+            return rc;
+        if (int rc = decode_launch(c, sl.d_wire, len, sl.d_fs, m, sl.d_wire, sl.d_info, sl.d_tiles, pp.kern))
+            return rc;
+        if (int rc = pipe_to_d2h(pp, sl))
             return rc;
         // copy back [lo, hi): bytes before lo belong to the previous segment
         const uint64_t back = hi - lo;
         if (out_pinned) {
-            WSG_HIP(hipMemcpyAsync(out + lo, sl.d_wire + (lo - base), back, hipMemcpyDeviceToHost, sl.stream));
+            WSG_HIP(hipMemcpyAsync(out + lo, sl.d_wire + (lo - base), back, hipMemcpyDeviceToHost, pp.d2h));
             sl.out_dst = nullptr;
         } else {
-            WSG_HIP(hipMemcpyAsync(sl.h_out, sl.d_wire + (lo - base), back, hipMemcpyDeviceToHost, sl.stream));
+            WSG_HIP(hipMemcpyAsync(sl.h_out, sl.d_wire + (lo - base), back, hipMemcpyDeviceToHost, pp.d2h));
             sl.out_dst = out + lo;
             sl.out_src = 0;
         }
         sl.out_len = back;
-        WSG_HIP(hipMemcpyAsync(sl.h_info, sl.d_info, m * sizeof(wsg_recv_info), hipMemcpyDeviceToHost, sl.stream));
+        WSG_HIP(hipMemcpyAsync(sl.h_info, sl.d_info, m * sizeof(wsg_recv_info), hipMemcpyDeviceToHost, pp.d2h));
         sl.info_dst = info + i0;
         sl.info_n = m;
         sl.base = base;
-        WSG_HIP(hipEventRecord(sl.done, sl.stream));
+        WSG_HIP(hipEventRecord(sl.done, pp.d2h));
         sl.busy = true;
     }
     for (auto& sl : c->slots)
@@ -675,10 +749,8 @@ namespace {
 int slot_reserve_enc(wsg_ctx::Slot& sl, uint64_t payload_bytes, uint64_t wire_bytes, uint32_t frames,
                      bool need_host)
 {
-    if (!sl.stream) {
-        WSG_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
-        WSG_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
-    }
+    if (int rc = slot_init(sl))
+        return rc;
     if (int rc = ensure_array(sl.d_payload, sl.payload_cap, payload_bytes + 32))
         return rc;
     if (int rc = ensure_array(sl.d_wire, sl.wire_cap, wire_bytes + 32))
@@ -809,23 +881,30 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
                 src = sl.h_in;
             }
         }
+        Pipe pp;
+        if (int rc = pipe_for(c, sl, pp))
+            return rc;
         if (plen)
-            WSG_HIP(hipMemcpyAsync(sl.d_payload, src, plen, hipMemcpyHostToDevice, sl.stream));
-        WSG_HIP(hipMemcpyAsync(sl.d_desc, sl.h_desc, m * sizeof(wsg_send_desc), hipMemcpyHostToDevice, sl.stream));
+            WSG_HIP(hipMemcpyAsync(sl.d_payload, src, plen, hipMemcpyHostToDevice, pp.h2d));
+        WSG_HIP(hipMemcpyAsync(sl.d_desc, sl.h_desc, m * sizeof(wsg_send_desc), hipMemcpyHostToDevice, pp.h2d));
+        if (int rc = pipe_to_kern(pp, sl))
+            return rc;
         const uint64_t wlen = wire_off[g.i1] - wire_off[g.i0];
-        if (int rc = encode_launch(c, sl.stream, sl.d_payload, sl.d_desc, m, sl.d_wire, wlen, sl.d_woff, sl.enc))
+        if (int rc = encode_launch(c, pp.kern, sl.d_payload, sl.d_desc, m, sl.d_wire, wlen, sl.d_woff, sl.enc))
+            return rc;
+        if (int rc = pipe_to_d2h(pp, sl))
             return rc;
         if (out_pinned) {
-            WSG_HIP(hipMemcpyAsync(wire + wire_off[g.i0], sl.d_wire, wlen, hipMemcpyDeviceToHost, sl.stream));
+            WSG_HIP(hipMemcpyAsync(wire + wire_off[g.i0], sl.d_wire, wlen, hipMemcpyDeviceToHost, pp.d2h));
             sl.out_dst = nullptr;
         } else {
-            WSG_HIP(hipMemcpyAsync(sl.h_out, sl.d_wire, wlen, hipMemcpyDeviceToHost, sl.stream));
+            WSG_HIP(hipMemcpyAsync(sl.h_out, sl.d_wire, wlen, hipMemcpyDeviceToHost, pp.d2h));
             sl.out_dst = wire + wire_off[g.i0];
             sl.out_src = 0;
         }
         sl.out_len = wlen;
         sl.info_n = 0;
-        WSG_HIP(hipEventRecord(sl.done, sl.stream));
+        WSG_HIP(hipEventRecord(sl.done, pp.d2h));
         sl.busy = true;
     }
     for (auto& sl : c->slots)

@@ -19,7 +19,10 @@ constexpr uint64_t PIECE = uint64_t(64) * CHUNK * EU;   // encode work piece: 4 
 #define WSG_FANOUT_FLAT 1
 #endif
 constexpr bool fanout_flat = WSG_FANOUT_FLAT != 0;       // fan-out: flat chunk stream (else per-frame pieces)
-constexpr int FAN_UNITS = 4;                             // fan-out: 16-B chunks per lane per pass
+#ifndef WSG_FAN_UNITS
+#define WSG_FAN_UNITS 4
+#endif
+constexpr int FAN_UNITS = WSG_FAN_UNITS;                 // fan-out: 16-B chunks per lane per pass
 constexpr int SCAN_PER_LANE = 4;
 constexpr uint64_t SCAN_ITEMS = uint64_t(BLOCK) * SCAN_PER_LANE;   // frames per scan block
 

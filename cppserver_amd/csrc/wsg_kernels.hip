@@ -1009,9 +1009,12 @@ __global__ __launch_bounds__(BLOCK) void k_fanout_flat(const uint8_t* __restrict
     const uint64_t data0 = f.data0;
     const uint32_t lane = threadIdx.x & 63;
 
-    if (blockIdx.x >= main_blocks) {
+    // edge blocks come first in the grid so that their longer per-lane work
+    // overlaps the streaming instead of trailing it
+    const uint32_t edge_blocks = gridDim.x - main_blocks;
+    if (blockIdx.x < edge_blocks) {
         // edge items: 2 per frame start (the last "start" is the wire's end)
-        const uint64_t item = uint64_t(blockIdx.x - main_blocks) * BLOCK + threadIdx.x;
+        const uint64_t item = uint64_t(blockIdx.x) * BLOCK + threadIdx.x;
         const uint64_t fr = item >> 1, h = item & 1;
         if (fr > k)
             return;
@@ -1031,7 +1034,8 @@ __global__ __launch_bounds__(BLOCK) void k_fanout_flat(const uint8_t* __restrict
 
     const uint64_t step = uint64_t(main_blocks) * (BLOCK / 64) * (64 * FU);
     const bool big = fsize >= uint64_t(64) * CHUNK;   // a 1 KiB pass row spans at most 2 frames
-    for (uint64_t base = (uint64_t(blockIdx.x) * (BLOCK / 64) + wave_id()) * (64 * FU); base < chunks; base += step) {
+    const uint32_t mb = blockIdx.x - edge_blocks;
+    for (uint64_t base = (uint64_t(mb) * (BLOCK / 64) + wave_id()) * (64 * FU); base < chunks; base += step) {
         if (fsize < CHUNK) {
             // several frames per chunk: byte by byte
 #pragma unroll 1

@@ -59,3 +59,13 @@ def frame_size(opcode, mask, length, status=0):
     body = length + (2 if prefix else 0)
     hdr = 2 if body < 126 else 4 if body < 65536 else 10
     return hdr + (4 if mask else 0) + body
+
+
+def frame_sizes(desc):
+    """frame_size over a SEND_DESC array, vectorized (uint64 per frame)."""
+    op = desc["opcode"].astype(np.uint64)
+    length = desc["len"].astype(np.uint64)
+    prefix = ((op & WS_CLOSE) == WS_CLOSE) & ((length > 0) | (desc["status"] != 0))
+    body = length + np.where(prefix, 2, 0).astype(np.uint64)
+    hdr = np.where(body < 126, 2, np.where(body < 65536, 4, 10)).astype(np.uint64)
+    return hdr + np.where(desc["mask"] != 0, 4, 0).astype(np.uint64) + body

@@ -99,6 +99,20 @@ int rx(int S, int F, size_t P, size_t chunk, int reps)
     }
     const double payload = double(S) * F * P;
     const bool ok = bytes == uint64_t(payload) * 2 * (reps + 1) && msgs == uint64_t(S) * F * 2 * (reps + 1);
+    if (!ok) {
+        int shown = 0;
+        for (int i = 0; i < S && shown < 5; ++i)
+            if (conns[i].messages != uint64_t(F) * 2 * (reps + 1) || conns[i].bytes != uint64_t(F) * P * 2 * (reps + 1)) {
+                std::fprintf(stderr, "rx: session %d got %llu messages / %llu bytes\n", i,
+                             (unsigned long long)conns[i].messages, (unsigned long long)conns[i].bytes);
+                ++shown;
+            }
+    }
+    if (!ok)
+        std::fprintf(stderr, "rx: delivered %llu bytes / %llu messages, expected %llu / %llu\n",
+                     (unsigned long long)bytes, (unsigned long long)msgs,
+                     (unsigned long long)(uint64_t(payload) * 2 * (reps + 1)),
+                     (unsigned long long)(uint64_t(S) * F * 2 * (reps + 1)));
     std::printf("{\"mode\": \"rx\", \"sessions\": %d, \"frames_per_session\": %d, \"payload\": %zu, \"feed_chunk\": %zu, "
                 "\"batched_GiBps\": %.3f, \"per_call_GiBps\": %.3f, \"batched_frames_per_s\": %.0f, "
                 "\"per_call_frames_per_s\": %.0f, \"delivered_ok\": %s}\n",

@@ -6,7 +6,9 @@
 //   hipcc --offload-arch=gfx950 -O3 -o membench membench.hip && ./membench [MiB]
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -250,6 +252,48 @@ int main(int argc, char** argv)
             run_wp<256, 8>("wave-piece 8K", src, dst, n16, cus, 16);
             run_wp<256, 16>("wave-piece 16K", src, dst, n16, cus, 8);
         }
+        CK(hipFree(src));
+        CK(hipFree(dst));
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "pcie") {
+        // PCIe ceilings with pinned host memory: H2D alone, D2H alone, and both
+        // directions at once on two streams (what a decode pipeline overlaps)
+        void *h_in, *h_out;
+        CK(hipHostMalloc(&h_in, bytes, hipHostMallocDefault));
+        CK(hipHostMalloc(&h_out, bytes, hipHostMallocDefault));
+        std::memset(h_in, 3, bytes);
+        hipStream_t s1, s2;
+        CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+        CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        auto timed = [&](const char* name, int mode, uint64_t seg) {
+            for (int warm = 0; warm < 2; ++warm) {
+                CK(hipDeviceSynchronize());
+                auto t0 = std::chrono::steady_clock::now();
+                for (uint64_t off = 0; off < bytes; off += seg) {
+                    const uint64_t n = std::min(seg, bytes - off);
+                    if (mode & 1)
+                        CK(hipMemcpyAsync((uint8_t*)src + off, (uint8_t*)h_in + off, n, hipMemcpyHostToDevice, s1));
+                    if (mode & 2)
+                        CK(hipMemcpyAsync((uint8_t*)h_out + off, (uint8_t*)dst + off, n, hipMemcpyDeviceToHost, s2));
+                }
+                CK(hipDeviceSynchronize());
+                const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                if (warm)
+                    printf("%-12s seg=%5llu MiB  %6.1f GiB/s per direction\n", name, (unsigned long long)(seg >> 20),
+                           bytes / sec / (1 << 30));
+            }
+        };
+        for (uint64_t seg : {uint64_t(8) << 20, uint64_t(32) << 20, bytes}) {
+            timed("H2D", 1, seg);
+            timed("D2H", 2, seg);
+            timed("H2D+D2H", 3, seg);
+        }
+        CK(hipHostFree(h_in));
+        CK(hipHostFree(h_out));
         CK(hipFree(src));
         CK(hipFree(dst));
         return 0;
