@@ -54,8 +54,16 @@ def dist_setup(args):
     if world > 1:
         import torch.distributed as dist
 
+        # $WSG_BENCH_BACKEND=gloo rehearses the N-rank path on fewer GPUs
+        # (ranks share devices round-robin); the real run is RCCL, one GPU per rank
+        backend = os.environ.get("WSG_BENCH_BACKEND", "nccl")
+        if backend != "nccl":
+            local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
     return rank, world, local

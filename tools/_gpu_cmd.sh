@@ -1,5 +1,3 @@
-mkdir -p gpurun_out/g12
-L=cppserver_amd/_build
-timeout -k 10 400 python -m pytest tests/test_gpu_parity.py -q -x -k "fanout" > gpurun_out/g12/t.log 2>&1 || exit $?
-CFG=c4 REPS=7 timeout -k 10 200 python tools/tune_enc.py $L/var/pieces/libwsg.so $L/libwsg.so $L/var/fu2/libwsg.so $L/var/fu8/libwsg.so > gpurun_out/g12/c4.log 2>&1
-CFG=c4 LEN=1000 KEYS=20000 timeout -k 10 200 python tools/tune_enc.py $L/libwsg.so $L/var/fu2/libwsg.so $L/var/fu8/libwsg.so >> gpurun_out/g12/c4.log 2>&1
+mkdir -p gpurun_out/g13
+WSG_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 10 --warmup 2 > gpurun_out/g13/dist2.json 2> gpurun_out/g13/dist2.err; echo "rc=$?" >> gpurun_out/g13/dist2.err
+timeout -k 10 600 python -m pytest tests/test_gpu_rx_batch.py -q -x -k repeated > gpurun_out/g13/rx.log 2>&1; echo "rc=$?" >> gpurun_out/g13/rx.log
