@@ -3,8 +3,8 @@
 
 Default (N=1) workload = BASELINE.json configs[1] ("C2"): unmask-only decode
 of 4096 masked binary frames x 64 KiB payload, one random key per frame,
-inputs resident in HBM.  One step = one wsg_decode_batch call (header unpack
-kernel + unmask kernel) over the whole batch.
+inputs resident in HBM.  One step = one wsg_decode_batch call over the whole
+batch = one k_decode launch (header unpack + unmask).
 
 N>1 (`torch.distributed.run --nproc-per-node N bench.py --gpus N`): one
 process per GPU; every rank decodes its own independent batch of the same
@@ -33,8 +33,8 @@ GIB = float(1 << 30)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--frames", type=int, default=None)
     ap.add_argument("--size", type=int, default=None)
@@ -126,8 +126,10 @@ class Workload:
             self.turn = 0
             self.info = torch.empty(n * ca.RECV_INFO.itemsize, dtype=torch.uint8, device=device)
             self.payload_bytes = n * size
-            self.alg_bytes = 2 * len(wire)           # unmask kernel: read wire + write out
-            self.kernel = "k_decode_unmask"
+            # k_decode: read wire + write out, plus per frame its start (8 B)
+            # and wsg_recv_info (32 B)
+            self.alg_bytes = 2 * len(wire) + n * 40
+            self.kernel = "k_decode"
             self.workload = "C2 unmask-only: %d masked binary frames x %d B payload, one key per frame" % (n, size)
             self.extra = {"frames": n, "payload_bytes_per_frame": size, "wire_bytes": len(wire)}
         elif self.cfg == "c3":
@@ -360,20 +362,33 @@ def main():
     codec.sync()
     ok = w.spot_check()
 
-    # HIP events around the dominant kernel of every 8th step: each event
-    # packet costs a few us, so timing every step would slow the step itself
-    codec.timing(True, every=8)
-    codec.timing_read(reset=True)
+    # Kernel time, live over the timed region, on the stream the kernels are
+    # launched on (torch's current stream).  C2 and C4 steps are ONE launch
+    # of the dominant kernel, so two events around the region give its
+    # average duration (launch gaps included: an upper bound) without adding
+    # anything between launches.  C3/C5 steps launch several kernels: HIP
+    # events around the dominant one of every 8th step (each event packet
+    # costs a few us, so timing every step would slow the step itself).
+    single = w.cfg in ("c2", "c4")
+    if not single:
+        codec.timing(True, every=8)
+        codec.timing_read(reset=True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    e0.record()
     for _ in range(args.steps):
         w.step()
+    e1.record()
     torch.cuda.synchronize()
     barrier(world)
     elapsed = time.perf_counter() - t0
-    kernel_ms, launches = codec.timing_read(reset=True)
-    codec.timing(False)
+    if single:
+        kernel_ms, launches = e0.elapsed_time(e1), args.steps
+    else:
+        kernel_ms, launches = codec.timing_read(reset=True)
+        codec.timing(False)
     codec.sync()
 
     elapsed = max_over_ranks(elapsed, world, device)
@@ -434,6 +449,8 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_launch": w.alg_bytes,
                 "avg_kernel_ms": round(k_avg_ms, 5),
+                "kernel_timing": ("HIP events around the timed region / steps (one launch per step)" if single
+                                  else "HIP events around every 8th launch in the timed region"),
             },
             "cpu_baseline": cpu1,
             "cpu_baseline_mt": cpu_mt,

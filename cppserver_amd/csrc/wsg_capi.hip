@@ -28,8 +28,6 @@ struct wsg_ctx {
     int blocks_per_cu = 32;   // measured best for the C2 unmask (tools/tune.py)
     unsigned long long* d_err = nullptr;
     // scratch
-    uint32_t* d_tiles = nullptr;
-    uint64_t tiles_cap = 0;
     wsg_enc_scratch enc;
     // staging for host entry points
     uint8_t* d_stage = nullptr;
@@ -54,8 +52,6 @@ struct wsg_ctx {
         uint64_t* d_fs = nullptr;
         wsg_recv_info* d_info = nullptr;
         uint64_t frames_cap = 0;
-        uint32_t* d_tiles = nullptr;
-        uint64_t tiles_cap = 0;
         // encode (wsg_encode_batch_host): payload in, frames out in d_wire
         uint8_t* d_payload = nullptr;
         uint64_t payload_cap = 0;
@@ -111,22 +107,6 @@ int grid_for(const wsg_ctx* c, uint64_t tiles)
 {
     const uint64_t cap = uint64_t(c->num_cus) * uint64_t(c->blocks_per_cu);
     return int(std::max<uint64_t>(1, std::min(tiles, cap)));
-}
-
-int ensure_tiles(wsg_ctx* c, uint64_t tiles)
-{
-    tiles = std::max<uint64_t>(tiles, 1);
-    if (tiles <= c->tiles_cap)
-        return WSG_OK;
-    WSG_HIP(hipDeviceSynchronize());
-    if (c->d_tiles)
-        WSG_HIP(hipFree(c->d_tiles));
-    c->d_tiles = nullptr;
-    c->tiles_cap = 0;
-    if (hipMalloc(&c->d_tiles, tiles * sizeof(uint32_t)) != hipSuccess)
-        return WSG_ENOMEM;
-    c->tiles_cap = tiles;
-    return WSG_OK;
 }
 
 void free_enc(wsg_enc_scratch& e)
@@ -300,7 +280,6 @@ int wsg_destroy(wsg_ctx* c)
         (void)hipEventDestroy(ev.b);
     }
     (void)hipFree(c->d_err);
-    (void)hipFree(c->d_tiles);
     free_enc(c->enc);
     (void)hipFree(c->d_stage);
     (void)hipFree(c->d_fs);
@@ -316,7 +295,6 @@ int wsg_destroy(wsg_ctx* c)
         if (sl.stream)
             (void)hipStreamSynchronize(sl.stream);
         (void)hipFree(sl.d_wire);
-        (void)hipFree(sl.d_tiles);
         (void)hipFree(sl.d_payload);
         (void)hipFree(sl.d_desc);
         (void)hipFree(sl.d_woff);
@@ -367,23 +345,22 @@ int wsg_sync(wsg_ctx* c, void* stream)
 
 namespace {
 
-// Device decode with explicit tile-map scratch (the pipelined host path runs
-// several of these concurrently, one per slot stream).
+// Device decode: one k_decode launch (the pipelined host path runs several
+// of these concurrently, one per slot).
 int decode_launch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const uint64_t* d_frame_start, uint32_t n,
-                  uint8_t* d_out, wsg_recv_info* d_info, uint32_t* d_tiles, hipStream_t s)
+                  uint8_t* d_out, wsg_recv_info* d_info, hipStream_t s)
 {
     if (n == 0) {
         if (wire_len && d_out != d_wire)
             WSG_HIP(hipMemcpyAsync(d_out, d_wire, wire_len, hipMemcpyDeviceToDevice, s));
         return WSG_OK;
     }
+    // every tile, and at least one block per 256 frames so that the frames of
+    // a short (or empty) wire are still checked
     const uint64_t tiles = ceil_div(wire_len, wsg::TILE);
-    WSG_HIP(wsg::launch_decode_parse(s, d_wire, wire_len, d_frame_start, n, d_info, d_tiles, tiles, c->d_err));
-    if (tiles == 0)
-        return WSG_OK;
     const int t = timing_begin(c, s);
-    WSG_HIP(wsg::launch_decode_unmask(s, grid_for(c, tiles), d_wire, d_out, wire_len, d_frame_start, d_info, n,
-                                      d_tiles, tiles));
+    WSG_HIP(wsg::launch_decode(s, grid_for(c, std::max(tiles, ceil_div(n, wsg::BLOCK))), d_wire, d_out, wire_len,
+                               d_frame_start, n, d_info, c->d_err));
     timing_end(c, s, t);
     return WSG_OK;
 }
@@ -397,9 +374,7 @@ int wsg_decode_batch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const
         return WSG_EINVAL;
     if (!aligned16(d_wire) || !aligned16(d_out))
         return WSG_EINVAL;
-    if (int rc = ensure_tiles(c, ceil_div(wire_len, wsg::TILE)))
-        return rc;
-    return decode_launch(c, d_wire, wire_len, d_frame_start, n, d_out, d_info, c->d_tiles, pick(c, stream));
+    return decode_launch(c, d_wire, wire_len, d_frame_start, n, d_out, d_info, pick(c, stream));
 }
 
 namespace {
@@ -562,8 +537,6 @@ int slot_reserve(wsg_ctx::Slot& sl, uint64_t bytes, uint64_t frames, bool need_h
         return rc;
     if (int rc = ensure_array(sl.d_wire, sl.wire_cap, bytes + 32))
         return rc;
-    if (int rc = ensure_array(sl.d_tiles, sl.tiles_cap, ceil_div(bytes + 32, wsg::TILE)))
-        return rc;
     if (frames > sl.frames_cap) {
         (void)hipFree(sl.d_fs);
         (void)hipFree(sl.d_info);
@@ -699,7 +672,7 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
         WSG_HIP(hipMemcpyAsync(sl.d_fs, sl.h_fs, m * sizeof(uint64_t), hipMemcpyHostToDevice, pp.h2d));
         if (int rc = pipe_to_kern(pp, sl))
             return rc;
-        if (int rc = decode_launch(c, sl.d_wire, len, sl.d_fs, m, sl.d_wire, sl.d_info, sl.d_tiles, pp.kern))
+        if (int rc = decode_launch(c, sl.d_wire, len, sl.d_fs, m, sl.d_wire, sl.d_info, pp.kern))
             return rc;
         if (int rc = pipe_to_d2h(pp, sl))
             return rc;

@@ -26,21 +26,16 @@ constexpr int FAN_UNITS = WSG_FAN_UNITS;                 // fan-out: 16-B chunks
 constexpr int SCAN_PER_LANE = 4;
 constexpr uint64_t SCAN_ITEMS = uint64_t(BLOCK) * SCAN_PER_LANE;   // frames per scan block
 
-__global__ void k_decode_parse(const uint8_t* wire, uint64_t wire_len, const uint64_t* fs, uint32_t n,
-                               wsg_recv_info* info, uint32_t* tile_first, uint64_t num_tiles,
-                               unsigned long long* err);
-__global__ void k_decode_unmask(const uint8_t* wire, uint8_t* out, uint64_t wire_len, const uint64_t* fs,
-                                const wsg_recv_info* info, uint32_t n, const uint32_t* tile_first,
-                                uint64_t num_tiles);
+__global__ void k_decode(const uint8_t* wire, uint8_t* out, uint64_t wire_len, const uint64_t* fs, uint32_t n,
+                         double frames_per_byte, uint32_t stride, wsg_recv_info* info, unsigned long long* err,
+                         uint64_t num_tiles);
 __global__ void k_xor(const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key, uint32_t phase);
 
 // Host launchers (defined in wsg_kernels.hip next to the kernels).
-hipError_t launch_decode_parse(hipStream_t s, const uint8_t* wire, uint64_t wire_len, const uint64_t* fs, uint32_t n,
-                               wsg_recv_info* info, uint32_t* tile_first, uint64_t num_tiles,
-                               unsigned long long* err);
-hipError_t launch_decode_unmask(hipStream_t s, int grid, const uint8_t* wire, uint8_t* out, uint64_t wire_len,
-                                const uint64_t* fs, const wsg_recv_info* info, uint32_t n,
-                                const uint32_t* tile_first, uint64_t num_tiles);
+// One-launch decode (k_decode): grid blocks over the wire's tiles, per-frame
+// info and the error latch from the same launch.
+hipError_t launch_decode(hipStream_t s, int grid, const uint8_t* wire, uint8_t* out, uint64_t wire_len,
+                         const uint64_t* fs, uint32_t n, wsg_recv_info* info, unsigned long long* err);
 // Sizes + piece counts scan (scan: 4 * ceil(n / SCAN_ITEMS) words), wire
 // offsets, piece starts (n + 1 each) and the piece -> frame map.
 hipError_t launch_encode_scan(hipStream_t s, const wsg_send_desc* desc, uint32_t n, uint64_t* wire_off,

@@ -11,14 +11,15 @@
 // Every output byte is written exactly once by an aligned 16-byte
 // nontemporal store (output is streamed, never re-read by the kernel).
 //
-// Three tile paths, chosen per tile (wave-uniform branch):
-//   stream   - the tile lies inside one payload: one 16-B load, four XORs
-//              with a tile-uniform rotated key, one 16-B store per step;
-//   boundary - the tile touches <= MAXF frames: their records are held in
-//              (scalar) registers and each 16-B chunk is classified against
-//              them; only chunks holding a header byte go byte-by-byte;
-//   dense    - more frames than that (tiny frames): per-chunk binary search
-//              of the frame table.
+// Decode is one launch (k_decode): each tile locates its frames itself with
+// scalar loads and takes one of three block-uniform paths:
+//   stream   - the tile lies inside one payload: 16-B load, XOR with the
+//              tile-rotated key, 16-B store;
+//   boundary - the tile touches <= MAXF frames: their payload segments are
+//              held in scalar registers; a chunk inside a segment XORs with
+//              its key word, the few chunks a segment edge cuts build masks;
+//   staged   - more frames (small frames): segments staged in LDS, 256
+//              frames per round.
 // No MFMA: XOR is not a contraction; the bound is HBM bandwidth.
 #include "wsg_internal.h"
 
@@ -47,7 +48,7 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #define WSG_DIAG_ENC 0   // timing-only encode diagnostics: 1 skip edge chunks, 2 no funnel
 #endif
 #ifndef WSG_DIAG
-#define WSG_DIAG 0   // 1/2: timing-only diagnostic builds of k_decode_unmask (tools/)
+#define WSG_DIAG 0   // 5: timing-only diagnostic build of k_decode (every tile streams; tools/)
 #endif
 #ifndef WSG_DIAG_FAN
 #define WSG_DIAG_FAN 0   // timing-only fan-out diagnostics: 1 no key loads, 2 no payload loads, 4 stores only
@@ -129,24 +130,11 @@ __device__ __forceinline__ void put_byte(v4u& w, uint32_t j, uint32_t b)
     w.w |= uint32_t(hi >> 32);
 }
 
-// v[j] for a runtime j < MAXF, as a select chain (no scratch).
-template <class V>
-__device__ __forceinline__ auto pick(V v, int j) -> decltype(v[0] + 0)
-{
-    auto r = v[0];
-    r = (j == 1) ? v[1] : r;
-    r = (j == 2) ? v[2] : r;
-    r = (j == 3) ? v[3] : r;
-    return r;
-}
-
 __device__ __forceinline__ void store_partial(uint8_t* dst, v4u w, uint32_t nbytes)
 {
     for (uint32_t j = 0; j < nbytes; ++j)
         dst[j] = uint8_t(lane_byte(w, j));
 }
-
-__device__ __forceinline__ uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
 constexpr int LDSF = BLOCK;   // frames a tile may touch and still take the LDS-staged path
 
@@ -157,7 +145,7 @@ __device__ __forceinline__ uint64_t lane_bcast(uint64_t v, int src)
     return uint64_t(lo) | (uint64_t(hi) << 32);
 }
 
-// tile_first[t] = frame for t in [lo, hi), for every lane's range, with the
+// map[t] = frame for t in [lo, hi) (encode: piece -> frame), for every lane's range, with the
 // whole wave storing each range (one lane per frame would serialise a large
 // frame's thousands of tiles on a single lane).
 __device__ __forceinline__ void fill_tiles_wave(uint32_t* tile_first, uint64_t lo, uint64_t hi, uint32_t frame)
@@ -179,21 +167,6 @@ __device__ __forceinline__ void fill_tiles_wave(uint32_t* tile_first, uint64_t l
 }
 
 __device__ __forceinline__ uint64_t lane_off(int u) { return (uint64_t(u) * BLOCK + threadIdx.x) * CHUNK; }
-
-// Last index in [lo, hi] whose start <= p; lo - 1 (possibly -1) if none.
-__device__ __forceinline__ int64_t owner_search(const uint64_t* start, int64_t lo, int64_t hi, uint64_t p)
-{
-    if (start[lo] > p)
-        return lo - 1;
-    while (lo < hi) {
-        const int64_t mid = lo + ((hi - lo + 1) >> 1);
-        if (start[mid] <= p)
-            lo = mid;
-        else
-            hi = mid - 1;
-    }
-    return lo;
-}
 
 // ---- wave / block exclusive scan of uint64 (wave64) ----------------------
 __device__ __forceinline__ uint64_t wave_inclusive_scan(uint64_t v)
@@ -231,271 +204,395 @@ __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total)
 } // namespace
 
 // ===========================================================================
-// Decode
+// Decode in one launch: k_decode
 // ===========================================================================
-
-// One lane per frame: header unpack (ws.cpp:320-386) from one 16-byte window
-// read, bounds checks, and the tile -> first-frame map of the unmask kernel.
-__global__ __launch_bounds__(BLOCK) void k_decode_parse(const uint8_t* __restrict__ wire, uint64_t wire_len,
-                                                        const uint64_t* __restrict__ fs, uint32_t n,
-                                                        wsg_recv_info* __restrict__ info,
-                                                        uint32_t* __restrict__ tile_first, uint64_t num_tiles,
-                                                        unsigned long long* err)
-{
-    if (blockIdx.x * BLOCK + (threadIdx.x & ~63u) >= n)
-        return;   // whole wave past the last frame
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    uint64_t lo_t = 0, hi_t = 0;
-    if (i < n) {
-        const uint64_t s = fs[i];
-        const uint64_t limit = (i + 1 < n) ? fs[i + 1] : wire_len;
-        wsg_recv_info r = {};
-        int e = WSG_ETRUNC;
-        if (s < wire_len) {
-            const uint64_t avail = wire_len - s;
-            const uint64_t a0 = s & ~uint64_t(15);
-            const v4u lo = ld16(wire + a0);
-            const v4u hi = (a0 + 16 < wire_len) ? ld16(wire + a0 + 16) : v4u{0, 0, 0, 0};
-            const v4u h = funnel(lo, hi, uint32_t(s & 15));   // wire[s .. s+16)
-            e = parse_header([&](uint32_t k) { return uint8_t(lane_byte(h, k)); }, avail, r);
-            if (e == 0) {
-                if (r.len > avail - r.hdr_len)
-                    e = WSG_ETRUNC;
-                else if (limit < s || limit - s < r.hdr_len || r.len > limit - s - r.hdr_len)
-                    e = WSG_EINVAL;   // the next frame starts inside this one
-            }
-        }
-        if (e != 0) {
-            r = wsg_recv_info{};
-            r.payload_off = s;
-            r.error = int8_t(e);
-            atomicMin(err, (static_cast<unsigned long long>(i) << 8) | static_cast<unsigned long long>(-e));
-        } else {
-            r.payload_off = s + r.hdr_len;
-        }
-        info[i] = r;
-        // tiles whose first byte falls in [s, next start) belong to frame i
-        lo_t = (i == 0) ? 0 : ceil_div(s, TILE);
-        hi_t = min((i + 1 < n) ? ceil_div(limit, TILE) : num_tiles, num_tiles);
-    }
-    fill_tiles_wave(tile_first, lo_t, hi_t, i);
-}
+//
+// Every tile finds its own frames.  The frame-start table is read-only and
+// sorted, so the tile's first frame is located with uniform (scalar) loads:
+// an interpolation guess, exact for equal-size frames, else a 16-ary search;
+// the headers of the (at most MAXF) frames the tile touches are parsed from
+// scalar loads of the wire.  Scalar loads do not queue behind the tile's
+// vector data loads (those return in issue order), so this metadata chain
+// overlaps the data's HBM latency.  The per-frame outputs (wsg_recv_info,
+// error latch) come from a lane-per-frame slice of the same launch.  One
+// launch instead of parse + unmask removes a kernel boundary: ~5 us per C2
+// batch (tools/tune.py, a build that skipped the parse launch).
+//
+// Tile paths (block-uniform): stream (inside one payload), boundary (<= MAXF
+// frames, records in scalar registers), staged (more frames: records staged
+// in LDS, LDSF frames per round).
 
 namespace {
 
-// Generic chunk of the unmask: owner by binary search, byte loop at frame
-// boundaries.  Used by dense tiles (many tiny frames) and the wire's tail.
-__device__ __forceinline__ void decode_chunk_generic(const uint8_t* __restrict__ wire, uint8_t* out, uint64_t wire_len,
-                                     const uint64_t* __restrict__ fs, const wsg_recv_info* __restrict__ info,
-                                     uint32_t n, uint32_t f, uint32_t f_hi, uint64_t p)
+// A wave-uniform value computed by vector instructions, moved to SGPRs.
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni(uint64_t x)
 {
-    int64_t o = owner_search(fs, f, f_hi, p);
-    uint64_t opoff = 0, oplen = 0;
-    uint32_t okey = 0;
-    if (o >= 0) {
-        opoff = info[o].payload_off;
-        oplen = info[o].len;
-        okey = info[o].key;
-        if (p >= opoff && p + CHUNK <= opoff + oplen) {
-            st16nt(out + p, ld16(wire + p) ^ key_rot(okey, uint32_t(p - opoff)));
-            return;
-        }
-    }
-    const uint32_t nb = uint32_t(min<uint64_t>(CHUNK, wire_len - p));
-    v4u src = {0, 0, 0, 0};
-    if (nb == CHUNK) {
-        src = ld16(wire + p);
-    } else {
-        for (uint32_t j = 0; j < nb; ++j)
-            put_byte(src, j, wire[p + j]);   // the wire's last partial chunk only
-    }
-    v4u w = {0, 0, 0, 0};
-    for (uint32_t j = 0; j < nb; ++j) {
-        const uint64_t q = p + j;
-        while (o + 1 < int64_t(n) && fs[o + 1] <= q) {
-            ++o;
-            opoff = info[o].payload_off;
-            oplen = info[o].len;
-            okey = info[o].key;
-        }
-        uint32_t b = lane_byte(src, j);
-        if (o >= 0 && q >= opoff && q - opoff < oplen)
-            b ^= key_byte(okey, q - opoff);
-        put_byte(w, j, b);
-    }
-    if (nb == CHUNK)
-        st16nt(out + p, w);
-    else
-        store_partial(out + p, w, nb);
+    return uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(x))) |
+           (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(x >> 32))) << 32);
 }
 
-// Records of the (at most MAXF) frames a boundary tile touches, as vector
-// values (kept in registers; MAXF == 4 == vector width).
-struct DecFrames {
-    v4u64 st;   // frame start (~0 when absent)
-    v4u64 po;   // payload start
-    v4u64 pe;   // payload end
-    v4u key;
-};
-static_assert(MAXF == 4, "frame records are 4-wide vectors");
-
-__device__ __forceinline__ int dec_owner(const DecFrames& F, uint64_t q)
+// Frame [s, limit) as PrepareReceiveFrame parses it when delivered whole
+// (ws.cpp:320-386), with the batch checks of wsg_decode_batch.  Returns 0 or
+// the frame's error; on error r describes an empty payload at s, so the
+// frame's bytes are copied.
+__device__ __forceinline__ int frame_parse(const uint8_t* __restrict__ wire, uint64_t wire_len, uint64_t s,
+                                           uint64_t limit, wsg_recv_info& r)
 {
-    int j = -1;
+    r = wsg_recv_info{};
+    int e = WSG_ETRUNC;
+    if (s < wire_len) {
+        const uint64_t avail = wire_len - s;
+        // wire[s .. s+16) as two u64 from the aligned 32-byte window, with
+        // 64-bit shifts only (scalar instructions when s is wave-uniform)
+        const uint64_t a0 = s & ~uint64_t(15);
+        const v4u lo = ld16(wire + a0);
+        const v4u hi = (a0 + 16 < wire_len) ? ld16(wire + a0 + 16) : v4u{0, 0, 0, 0};
+        uint64_t q0 = uint64_t(lo.x) | (uint64_t(lo.y) << 32), q1 = uint64_t(lo.z) | (uint64_t(lo.w) << 32);
+        const uint64_t q2 = uint64_t(hi.x) | (uint64_t(hi.y) << 32), q3 = uint64_t(hi.z) | (uint64_t(hi.w) << 32);
+        uint64_t q2s = q2;
+        if (s & 8) {
+            q0 = q1;
+            q1 = q2;
+            q2s = q3;
+        }
+        const uint32_t b = 8u * uint32_t(s & 7);
+        const uint64_t h0 = b ? (q0 >> b) | (q1 << (64u - b)) : q0;
+        const uint64_t h1 = b ? (q1 >> b) | (q2s << (64u - b)) : q1;
+        e = parse_header([&](uint32_t k) { return uint8_t(k < 8 ? h0 >> (8u * k) : h1 >> (8u * (k - 8))); }, avail, r);
+        if (e == 0) {
+            if (r.len > avail - r.hdr_len)
+                e = WSG_ETRUNC;
+            else if (limit < s || limit - s < r.hdr_len || r.len > limit - s - r.hdr_len)
+                e = WSG_EINVAL;   // the next frame starts inside this one
+        }
+    }
+    if (e != 0) {
+        r = wsg_recv_info{};
+        r.payload_off = s;
+        r.error = int8_t(e);
+    } else {
+        r.payload_off = s + r.hdr_len;
+    }
+    return e;
+}
+
+__device__ __forceinline__ uint64_t fs_at(const uint64_t* __restrict__ fs, uint32_t n, int64_t i)
+{
+    return fs[min<int64_t>(i, int64_t(n) - 1)];   // clamped: the load never depends on a compare
+}
+
+// Last index i < b with fs[i] <= p, or a - 1, given fs[a - 1] <= p < fs[b]
+// (fs[-1] = -inf, fs[n] = +inf): 8 independent probes per round (one round
+// of scalar loads when a/b are uniform); ends for any table.
+__device__ __forceinline__ int64_t search8(const uint64_t* __restrict__ fs, uint32_t a, uint32_t b, uint64_t p)
+{
+    while (a < b) {
+        const uint32_t step = (b - a + 8) / 9;   // probes a - 1 + step * k, k = 1..8 (< b)
+        uint64_t v[8];
 #pragma unroll
-    for (int k = 0; k < MAXF; ++k)
-        j = (F.st[k] <= q) ? k : j;
-    return j;
+        for (int k = 0; k < 8; ++k)
+            v[k] = fs[min(a - 1 + step * (k + 1), b - 1)];
+        uint32_t na = a, nb = b;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t ix = min(a - 1 + step * (k + 1), b - 1);
+            if (ix >= na && ix < nb) {
+                if (v[k] <= p)
+                    na = ix + 1;
+                else
+                    nb = ix;
+            }
+        }
+        a = na;
+        b = nb;
+    }
+    return int64_t(a) - 1;
+}
+
+// The frames a tile touches: first = max(f0, 0), where f0 is the last frame
+// starting at or before the tile's first byte (-1: none); st[k] = fs[first+k]
+// (~0 past the table).
+struct TileLoc {
+    int64_t f0;
+    uint32_t first;
+    uint64_t st[MAXF + 1];
+};
+
+// The tile's first-frame guess (exact for equal-size frames).
+__device__ __forceinline__ uint64_t tile_guess(uint32_t n, double frames_per_byte, uint64_t base)
+{
+    return uni(min(uint64_t(double(base) * frames_per_byte), uint64_t(n - 1)));
+}
+
+// Lane k's entry of the coarse probe around the guess g: fs[g + (k - 32) S].
+__device__ __forceinline__ uint32_t probe_index(uint64_t g, uint32_t stride, uint32_t n, int k)
+{
+    const int64_t i = int64_t(g) + int64_t(k - 32) * int64_t(stride);
+    return uint32_t(max<int64_t>(0, min<int64_t>(i, int64_t(n) - 1)));
+}
+
+// Locate the tile's frames.  `probe` is this lane's coarse-probe entry,
+// loaded before the tile's data (so it is back first).  Equal-size frames
+// hit the guess (one round of scalar loads); otherwise the probe brackets
+// the answer to `stride` frames (a miss outside +-32 strides searches the
+// rest of the table), and search8 finishes it.
+__device__ __forceinline__ void locate(const uint64_t* __restrict__ fs, uint32_t n, uint64_t g, uint32_t stride,
+                                       uint64_t probe, uint64_t base, TileLoc& L)
+{
+    const uint64_t below = __ballot(probe <= base);   // a prefix of the lanes for a sorted table
+    uint64_t w[MAXF + 2];
+#pragma unroll
+    for (int k = 0; k < MAXF + 2; ++k) {
+        const uint64_t x = fs_at(fs, n, int64_t(g) + k);
+        w[k] = (g + k < n) ? x : ~uint64_t(0);
+    }
+    if (w[0] <= base && base < w[1]) {   // the guess (equal-size frames)
+        L.f0 = int64_t(g);
+        L.first = uint32_t(g);
+#pragma unroll
+        for (int k = 0; k <= MAXF; ++k)
+            L.st[k] = w[k];
+        return;
+    }
+    // candidates [a, b) for the last start <= base, fs[a - 1] <= base < fs[b]
+    const int m = __builtin_popcountll(below);
+    uint32_t a = m > 0 ? probe_index(g, stride, n, m - 1) + 1 : 0;
+    uint32_t b = m < 64 ? probe_index(g, stride, n, m) : n;
+    if (m == 0 && probe_index(g, stride, n, 0) == 0)
+        b = 0;   // even fs[0] is past base: no frame starts at or before it
+    L.f0 = search8(fs, a, b, base);
+    L.first = uint32_t(L.f0 < 0 ? 0 : L.f0);
+#pragma unroll
+    for (int k = 0; k <= MAXF; ++k) {
+        const uint64_t x = fs_at(fs, n, int64_t(L.first) + k);
+        L.st[k] = (uint64_t(L.first) + k < n) ? x : ~uint64_t(0);
+    }
+}
+
+// Store chunk [p, p + 16) of a tile ending at tend (partial at the wire's end).
+__device__ __forceinline__ void store_chunk(uint8_t* out, uint64_t p, uint64_t tend, v4u w)
+{
+    if (p + CHUNK <= tend)
+        st16nt(out + p, w);
+    else if (p < tend)
+        store_partial(out + p, w, uint32_t(tend - p));
+}
+
+// A frame's payload as seen from one tile: bytes [lo, hi) of the tile
+// (tile-relative, clamped to the tile; for the frames of a tile in order,
+// lo and hi are non-decreasing) XOR with kr, the frame's key rotated
+// to the tile's phase — chunk offsets are multiples of 16, so one rotation
+// serves every chunk of the tile (ws.cpp:403: byte i uses key[i % 4]).
+struct Seg {
+    uint32_t lo, hi, kr;
+};
+
+__device__ __forceinline__ Seg tile_seg(uint64_t po, uint64_t pe, uint32_t key, uint64_t base, uint32_t span)
+{
+    Seg s;
+    s.lo = po <= base ? 0u : uint32_t(min<uint64_t>(po - base, span));
+    s.hi = pe <= base ? 0u : uint32_t(min<uint64_t>(pe - base, span));
+    if (s.hi < s.lo)
+        s.hi = s.lo;   // empty stays at its place: segment ends stay sorted
+    s.kr = key_rot(key, uint32_t(base - po));   // (base - po) mod 4, also when po > base
+    return s;
+}
+
+// Bytes [0, k) of a dword as a mask (k <= 0: none, k >= 4: all).
+__device__ __forceinline__ uint32_t low_bytes(int k)
+{
+    return k <= 0 ? 0u : k >= 4 ? ~0u : (1u << (8 * k)) - 1u;
+}
+
+// The XOR word of segment s for the chunk at tile offset o (zero outside s).
+__device__ __forceinline__ v4u seg_xor(uint32_t o, const Seg& s)
+{
+    if (s.hi <= o || s.lo >= o + CHUNK)
+        return v4u{0, 0, 0, 0};
+    const int a = s.lo > o ? int(s.lo - o) : 0;
+    const int b = s.hi < o + CHUNK ? int(s.hi - o) : int(CHUNK);
+    v4u m;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+        m[d] = s.kr & low_bytes(b - 4 * d) & ~low_bytes(a - 4 * d);
+    return m;
 }
 
 } // namespace
 
-// Unmask (ws.cpp:399-406): out = wire with every payload XORed by its key.
-__global__ __launch_bounds__(BLOCK) void k_decode_unmask(const uint8_t* __restrict__ wire, uint8_t* out,
-                                                         uint64_t wire_len, const uint64_t* __restrict__ fs,
-                                                         const wsg_recv_info* __restrict__ info, uint32_t n,
-                                                         const uint32_t* __restrict__ tile_first,
-                                                         uint64_t num_tiles)
+// Decode (ws.cpp:320-406 over a batch): out = wire with every payload XORed
+// by its key; info[i] and the error latch per frame.
+__global__ __launch_bounds__(BLOCK) void k_decode(const uint8_t* __restrict__ wire, uint8_t* out, uint64_t wire_len,
+                                                  const uint64_t* __restrict__ fs, uint32_t n, double frames_per_byte,
+                                                  uint32_t stride, wsg_recv_info* __restrict__ info,
+                                                  unsigned long long* err, uint64_t num_tiles)
 {
+    // per-frame slice: header unpack + checks, one lane per frame
+    const uint64_t fstride = uint64_t(gridDim.x) * BLOCK;
+    for (uint64_t i0 = uint64_t(blockIdx.x) * BLOCK + (threadIdx.x & ~63u); i0 < n; i0 += fstride) {
+        const uint64_t i = i0 + (threadIdx.x & 63u);
+        if (i < n) {
+            wsg_recv_info r;
+            const int e = frame_parse(wire, wire_len, fs[i], i + 1 < n ? fs[i + 1] : wire_len, r);
+            if (e != 0)
+                atomicMin(err, (static_cast<unsigned long long>(i) << 8) | static_cast<unsigned long long>(-e));
+            info[i] = r;
+        }
+    }
+
     for (uint64_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
         const uint64_t base = t * TILE;
         const uint64_t tend = min(base + TILE, wire_len);
-        const uint32_t f = min(tile_first[t], n - 1);
-        uint32_t f_hi = (t + 1 < num_tiles) ? min(tile_first[t + 1], n - 1) : n - 1;
-        f_hi = max(f, f_hi);   // f_hi < f only with invalid (non-monotone) frame starts
+        const uint32_t span = uint32_t(tend - base);
+        const bool full = span == TILE;
 
-        if (tend - base != TILE) {
-            // the wire's last, partial tile
-#pragma unroll 1
-            for (int u = 0; u < UNROLL; ++u) {
-                const uint64_t p = base + lane_off(u);
-                if (p < tend)
-                    decode_chunk_generic(wire, out, wire_len, fs, info, n, f, f_hi, p);
-            }
-            continue;
-        }
+        // coarse probe of the frame table (vector load, issued before the
+        // data loads: loads return in issue order)
+        const uint64_t g = tile_guess(n, frames_per_byte, base);
+        const uint64_t probe = fs[probe_index(g, stride, n, int(threadIdx.x & 63))];
+        __builtin_amdgcn_sched_barrier(0);
 
-        // the tile's data does not depend on frame metadata: issue it first
+        // the tile's data does not depend on frame metadata: issue it next
+        // (the wire's last tile reads whole 16-B blocks up to its end)
         v4u v[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u)
-            v[u] = ld16nt(wire + base + lane_off(u));
-
-#if WSG_DIAG == 2   // diagnostic build (timing only, wrong output): no metadata at all
-        {
+        if (full) {
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u)
-                st16nt(out + base + lane_off(u), v[u] ^ uint32_t(t));
-            continue;
-        }
-#endif
-        const uint64_t poff = info[f].payload_off;
-        const uint64_t pend = poff + info[f].len;
-        const uint32_t key = info[f].key;
-#if WSG_DIAG == 1   // diagnostic build (timing only, wrong output): every tile streams
-        if (true) {
-#else
-        if (base >= poff && tend <= pend) {
-#endif
-            // stream: the whole tile is payload of frame f
-            const uint32_t k = key_rot(key, uint32_t(base - poff));
+                v[u] = ld16nt(wire + base + lane_off(u));
+        } else {
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u)
-                st16nt(out + base + lane_off(u), v[u] ^ k);
-            continue;
+                v[u] = (lane_off(u) < span) ? ld16(wire + base + lane_off(u)) : v4u{0, 0, 0, 0};
         }
 
-        if (f_hi - f < MAXF) {
-            // boundary: frames f..f_hi from registers
-            DecFrames F;
+        TileLoc L;
+        locate(fs, n, g, stride, probe, base, L);
+        // frames touching the tile: a prefix of first, first + 1, ...
+        int c = 0;
+#pragma unroll
+        for (int k = 0; k <= MAXF; ++k) {
+            const bool touches = uint64_t(L.first) + k < n && (k == 0 ? L.f0 >= 0 || L.st[0] < tend : L.st[k] < tend);
+            if (touches && c == k)
+                c = k + 1;
+        }
+
+        if (WSG_DIAG == 5 || c <= MAXF) {
+            // frames' payload segments in scalar registers
+            Seg S[MAXF];
 #pragma unroll
             for (int k = 0; k < MAXF; ++k) {
-                if (f + k <= f_hi) {
-                    F.st[k] = fs[f + k];
-                    F.po[k] = info[f + k].payload_off;
-                    F.pe[k] = F.po[k] + info[f + k].len;
-                    F.key[k] = info[f + k].key;
-                } else {
-                    F.st[k] = ~uint64_t(0);
-                    F.po[k] = F.pe[k] = 0;
-                    F.key[k] = 0;
+                S[k] = Seg{0, 0, 0};
+                if (k < c) {
+                    wsg_recv_info r;
+                    const uint64_t lim = (uint64_t(L.first) + k + 1 < n) ? L.st[k + 1] : wire_len;
+                    frame_parse(wire, wire_len, L.st[k], lim, r);
+                    const Seg g = tile_seg(r.payload_off, r.payload_off + r.len, r.key, base, span);
+                    S[k] = Seg{uni(g.lo), uni(g.hi), uni(g.kr)};
                 }
             }
+#if WSG_DIAG == 5   // timing-only: every tile streams with its first frame's key (8-wave register budget)
+            if (true) {
+#else
+            if (full && S[0].lo == 0 && S[0].hi == TILE) {
+#endif
+                // stream: the whole tile is payload of one frame
+#pragma unroll
+                for (int u = 0; u < UNROLL; ++u)
+                    st16nt(out + base + lane_off(u), v[u] ^ S[0].kr);
+                continue;
+            }
+            // boundary: per chunk, the key word of the segment holding it;
+            // the few chunks a segment edge cuts build byte masks
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
-                const uint64_t p = base + lane_off(u);
-                const int j = dec_owner(F, p);
-                const uint64_t po = pick(F.po, j < 0 ? 0 : j), pe = pick(F.pe, j < 0 ? 0 : j);
-                if (j >= 0 && p >= po && p + CHUNK <= pe) {
-                    st16nt(out + p, v[u] ^ key_rot(pick(F.key, j), uint32_t(p - po)));
-                } else {
-                    v4u w = v[u];
+                const uint32_t o = uint32_t(lane_off(u));
+                uint32_t kx = 0;
+                bool cut = false;
 #pragma unroll
-                    for (uint32_t b = 0; b < CHUNK; ++b) {
-                        const uint64_t q = p + b;
-                        const int jb = dec_owner(F, q);
-                        const int jc = jb < 0 ? 0 : jb;
-                        const uint64_t qo = pick(F.po, jc);
-                        if (jb >= 0 && q >= qo && q < pick(F.pe, jc))
-                            w[b >> 2] ^= uint32_t(key_byte(pick(F.key, jc), q - qo)) << (8u * (b & 3u));
-                    }
-                    st16nt(out + p, w);
+                for (int k = 0; k < MAXF; ++k) {
+                    kx = (S[k].lo <= o && o + CHUNK <= S[k].hi) ? S[k].kr : kx;
+                    cut |= (S[k].lo > o && S[k].lo < o + CHUNK) || (S[k].hi > o && S[k].hi < o + CHUNK);
                 }
+                v4u x = v4u{kx, kx, kx, kx};
+                if (cut) {
+                    x = seg_xor(o, S[0]);
+#pragma unroll
+                    for (int k = 1; k < MAXF; ++k)
+                        x |= seg_xor(o, S[k]);
+                }
+                store_chunk(out, base + o, tend, v[u] ^ x);
             }
             continue;
         }
 
-        if (f_hi - f < LDSF) {
-            // many frames: stage their records in LDS, binary-search per chunk
-            __shared__ uint64_t s_st[LDSF], s_po[LDSF], s_pe[LDSF];
-            __shared__ uint32_t s_key[LDSF];
-            const int cnt = int(f_hi - f) + 1;
-            __syncthreads();   // the previous tile's readers are done
+        // staged: payload segments in LDS, LDSF frames per round
+        __shared__ uint32_t s_lo[LDSF], s_hi[LDSF], s_kr[LDSF];
+        // stage the segments of frames r0, r0 + 1, ... that touch the tile;
+        // more = frames past the stage touch it too (block-uniform)
+        auto stage = [&](uint64_t r0, int& cnt, bool& more) {
+            const uint64_t fi = r0 + threadIdx.x;
+            uint64_t sj = ~uint64_t(0), lim = wire_len;
+            if (fi < n) {
+                sj = fs[fi];
+                lim = fi + 1 < n ? fs[fi + 1] : wire_len;
+            }
+            // frame `first` touches (c > MAXF); the others when they start in the tile
+            const bool touch = fi < n && (fi == L.first || sj < tend);
+            __syncthreads();   // the previous readers are done with the stage
+            cnt = __syncthreads_count(touch);
+            more = __syncthreads_or(threadIdx.x == LDSF - 1 && touch && fi + 1 < n && lim < tend);
             if (int(threadIdx.x) < cnt) {
-                const uint32_t k = f + threadIdx.x;
-                s_st[threadIdx.x] = fs[k];
-                s_po[threadIdx.x] = info[k].payload_off;
-                s_pe[threadIdx.x] = info[k].payload_off + info[k].len;
-                s_key[threadIdx.x] = info[k].key;
+                wsg_recv_info r;
+                frame_parse(wire, wire_len, sj, lim, r);
+                const Seg g = tile_seg(r.payload_off, r.payload_off + r.len, r.key, base, span);
+                s_lo[threadIdx.x] = g.lo;
+                s_hi[threadIdx.x] = g.hi;
+                s_kr[threadIdx.x] = g.kr;
             }
             __syncthreads();
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const uint64_t p = base + lane_off(u);
-                int j = -1;
-                if (s_st[0] <= p) {
-                    int lo = 0, hi = cnt - 1;
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (s_st[mid] <= p)
-                            lo = mid;
-                        else
-                            hi = mid - 1;
-                    }
-                    j = lo;
-                }
-                if (j >= 0 && p >= s_po[j] && p + CHUNK <= s_pe[j]) {
-                    st16nt(out + p, v[u] ^ key_rot(s_key[j], uint32_t(p - s_po[j])));
-                } else {
-                    v4u w = v[u];
-#pragma unroll
-                    for (uint32_t b = 0; b < CHUNK; ++b) {
-                        const uint64_t q = p + b;
-                        while (j + 1 < cnt && s_st[j + 1] <= q)
-                            ++j;
-                        if (j >= 0 && q >= s_po[j] && q < s_pe[j])
-                            w[b >> 2] ^= uint32_t(key_byte(s_key[j], q - s_po[j])) << (8u * (b & 3u));
-                    }
-                    st16nt(out + p, w);
-                }
+        };
+        // XOR words of the staged segments for the chunk at tile offset o
+        auto chunk_xor = [&](uint32_t o, int cnt) {
+            int lo = 0, hi = cnt;   // first segment ending after o (segment ends are non-decreasing)
+#pragma unroll 1
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_hi[mid] <= o)
+                    lo = mid + 1;
+                else
+                    hi = mid;
             }
+            v4u x = {0, 0, 0, 0};
+#pragma unroll 1
+            for (int j = lo; j < cnt && s_lo[j] < o + CHUNK; ++j)
+                x |= seg_xor(o, Seg{s_lo[j], s_hi[j], s_kr[j]});
+            return x;
+        };
+        int cnt;
+        bool more;
+        stage(L.first, cnt, more);
+        if (!more) {
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u)
+                store_chunk(out, base + lane_off(u), tend, v[u] ^ chunk_xor(uint32_t(lane_off(u)), cnt));
             continue;
         }
-
-        // dense: more frames than the LDS stage holds (tiny frames)
+        // more than LDSF frames touch the tile (tiny frames): chunk by chunk,
+        // every round restaged, the data re-read
 #pragma unroll 1
-        for (int u = 0; u < UNROLL; ++u)
-            decode_chunk_generic(wire, out, wire_len, fs, info, n, f, f_hi, base + lane_off(u));
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint32_t o = uint32_t(lane_off(u));
+            v4u x = {0, 0, 0, 0};
+            for (uint64_t r0 = L.first;; r0 += LDSF) {
+                stage(r0, cnt, more);
+                x |= chunk_xor(o, cnt);
+                if (!more)
+                    break;
+            }
+            const v4u d = o < span ? ld16(wire + base + o) : v4u{0, 0, 0, 0};
+            store_chunk(out, base + o, tend, d ^ x);
+        }
     }
 }
 
@@ -1118,20 +1215,20 @@ __global__ __launch_bounds__(BLOCK) void k_xor(const uint8_t* src, uint8_t* dst,
 // Host launchers
 // ===========================================================================
 
-hipError_t launch_decode_parse(hipStream_t s, const uint8_t* wire, uint64_t wire_len, const uint64_t* fs, uint32_t n,
-                               wsg_recv_info* info, uint32_t* tile_first, uint64_t num_tiles,
-                               unsigned long long* err)
+hipError_t launch_decode(hipStream_t s, int grid, const uint8_t* wire, uint8_t* out, uint64_t wire_len,
+                         const uint64_t* fs, uint32_t n, wsg_recv_info* info, unsigned long long* err)
 {
-    const uint32_t grid = (n + BLOCK - 1) / BLOCK;
-    k_decode_parse<<<grid, BLOCK, 0, s>>>(wire, wire_len, fs, n, info, tile_first, num_tiles, err);
-    return hipGetLastError();
-}
-
-hipError_t launch_decode_unmask(hipStream_t s, int grid, const uint8_t* wire, uint8_t* out, uint64_t wire_len,
-                                const uint64_t* fs, const wsg_recv_info* info, uint32_t n,
-                                const uint32_t* tile_first, uint64_t num_tiles)
-{
-    k_decode_unmask<<<grid, BLOCK, 0, s>>>(wire, out, wire_len, fs, info, n, tile_first, num_tiles);
+    const uint64_t tiles = (wire_len + TILE - 1) / TILE;
+    // frames per wire byte: the tile's first-frame guess (exact for equal-size frames)
+    const double fpb = wire_len ? double(n) / double(wire_len) : 0.0;
+    // coarse-probe stride: 64 probes span +-32 strides around the guess, a
+    // power of two >= sqrt(n) / 32 frames (a random-walk deviation of frame
+    // counts from the guess grows like sqrt(n): C3's 65536 ragged frames
+    // deviate by ~100)
+    uint32_t stride = 1;
+    while (uint64_t(stride) * stride * 1024 < n)
+        stride <<= 1;
+    k_decode<<<grid, BLOCK, 0, s>>>(wire, out, wire_len, fs, n, fpb, stride, info, err, tiles);
     return hipGetLastError();
 }
 

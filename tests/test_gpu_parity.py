@@ -165,6 +165,57 @@ def test_encode_mixed_vs_oracle(codec, lo, hi, n):
     assert_decode_parity(codec, wire_o, off_o[:-1])
 
 
+# ------------------------------------------- k_decode tile paths (one launch)
+def _frames_wire(rng, lens, gaps=None, lead=0):
+    """Masked/unmasked frames of the given payload lengths back to back, with
+    optional junk gaps before each frame (gap bytes are copied by decode)."""
+    payload, desc = _mixed_desc(rng, len(lens), 0, 0)
+    desc["len"] = lens
+    desc["src_off"] = 0
+    desc["status"] = 0
+    payload = wl.random_bytes(rng, int(max(lens.max(), 1)) + 16)
+    wire_o, off_o = oracle.encode_batch(payload, desc)
+    parts, fs, at = [], [], 0
+    junk = lambda k: wl.random_bytes(rng, k)
+    if lead:
+        parts.append(junk(lead))
+        at += lead
+    for i in range(len(lens)):
+        g = int(gaps[i]) if gaps is not None else 0
+        if g:
+            parts.append(junk(g))
+            at += g
+        f = wire_o[int(off_o[i]): int(off_o[i + 1])]
+        fs.append(at)
+        parts.append(f)
+        at += len(f)
+    return np.concatenate(parts), np.array(fs, dtype=np.uint64)
+
+
+@pytest.mark.parametrize("case", ["tiny-then-huge", "huge-then-tiny", "empty-mix", "gaps", "lead-gap",
+                                  "tile-edges"])
+def test_decode_tile_paths_vs_oracle(codec, case):
+    rng = np.random.default_rng(sum(map(ord, case)))
+    gaps, lead = None, 0
+    if case == "tiny-then-huge":      # the interpolation guess misses: searched tiles
+        lens = np.concatenate([rng.integers(0, 20, 3000), rng.integers(60000, 200000, 40)])
+    elif case == "huge-then-tiny":
+        lens = np.concatenate([rng.integers(60000, 200000, 40), rng.integers(0, 20, 3000)])
+    elif case == "empty-mix":         # empty payloads between large and small frames (staged tiles)
+        lens = rng.choice([0, 0, 0, 1, 5, 300, 20000], 4000)
+    elif case == "gaps":
+        lens = rng.integers(0, 5000, 800)
+        gaps = rng.integers(0, 40, 800) * (rng.random(800) < 0.5)
+    elif case == "lead-gap":          # the first tiles have no frame start at or before them
+        lens = rng.integers(100, 3000, 200)
+        lead = 40000
+    else:                             # frame starts on and next to 16 KiB tile edges
+        lens = np.array([16384 - 14, 16384 - 6, 16384 - 2, 16384 - 15, 1, 16384 * 3 - 14, 0, 16384 - 8] * 8)
+    wire, fs = _frames_wire(rng, lens.astype(np.uint64), gaps, lead)
+    assert_decode_parity(codec, wire, fs)
+    assert_decode_parity(codec, wire, fs, inplace=True)
+
+
 def test_c3_roundtrip_full_size(codec):
     """C3 at BASELINE size (65536 frames, 128 B-64 KiB): encode -> decode on the
     GPU returns every payload byte (size-independent property), plus oracle

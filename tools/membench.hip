@@ -230,6 +230,141 @@ void run(const char* name, const u32x4* src, u32x4* dst, uint64_t n16, int cus, 
     CK(hipEventDestroy(b));
 }
 
+// Read-only stream: XOR-reduce into one dword per lane, stored only if it
+// hits an impossible value (keeps the loads alive).
+template <int U>
+__global__ __launch_bounds__(256) void k_read(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n16)
+{
+    const uint64_t per_tile = 256ull * U;
+    const uint64_t tiles = n16 / per_tile;
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            acc ^= __builtin_nontemporal_load(src + t * per_tile + uint64_t(u) * 256 + threadIdx.x);
+    }
+    if (acc.x == 0xdeadbeefu && acc.y == 0x01234567u)
+        dst[threadIdx.x] = acc;
+}
+
+// Streaming copy-with-XOR with the whole tile's loads issued before any
+// store (same as k_stream U) but software-pipelined: the loads of tile t+grid
+// are issued before the stores of tile t.
+template <int U>
+__global__ __launch_bounds__(256) void k_pipe(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n16,
+                                              uint32_t key)
+{
+    const uint64_t per_tile = 256ull * U;
+    const uint64_t tiles = n16 / per_tile;
+    uint64_t t = blockIdx.x;
+    if (t >= tiles)
+        return;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        v[u] = __builtin_nontemporal_load(src + t * per_tile + uint64_t(u) * 256 + threadIdx.x);
+    for (;;) {
+        const uint64_t nt = t + gridDim.x;
+        const uint64_t lt = nt < tiles ? nt : t;   // last pass re-reads its own tile
+        u32x4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            w[u] = __builtin_nontemporal_load(src + lt * per_tile + uint64_t(u) * 256 + threadIdx.x);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_nontemporal_store(v[u] ^ key, dst + t * per_tile + uint64_t(u) * 256 + threadIdx.x);
+        if (nt >= tiles)
+            break;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            v[u] = w[u];
+        t = nt;
+    }
+}
+
+template <class F>
+double time_kernel(F launch, int reps = 20)
+{
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i)
+        launch(i);
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i)
+        launch(i);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    CK(hipEventDestroy(a));
+    CK(hipEventDestroy(b));
+    return ms / reps;
+}
+
+// Ceiling exploration at a C2-sized footprint: read-only, write-only,
+// out-of-place copy with the destination at several offsets from the source
+// (channel/bank aliasing), in-place, software-pipelined copy.
+static int explore(uint64_t bytes, int cus)
+{
+    const uint64_t n16 = bytes / 16;
+    const uint64_t span = 4 * bytes + (64ull << 20);
+    uint8_t* base;
+    CK(hipMalloc(&base, span));
+    CK(hipMemset(base, 5, span));
+    auto P = [&](uint64_t off) { return (u32x4*)(base + off); };
+    auto gbs = [&](double ms, double mult) { return mult * bytes / (ms * 1e-3) / 1e9; };
+    for (int bpc : {8, 16, 32}) {
+        const int grid = cus * bpc;
+        double ms = time_kernel([&](int i) { k_read<4><<<grid, 256>>>(P((i & 1) * 2 * bytes), P(span - 4096), n16); });
+        printf("read-only U=4 bpc=%2d      %8.1f us  %7.1f GB/s\n", bpc, ms * 1e3, gbs(ms, 1));
+        ms = time_kernel([&](int i) { k_read<8><<<grid, 256>>>(P((i & 1) * 2 * bytes), P(span - 4096), n16); });
+        printf("read-only U=8 bpc=%2d      %8.1f us  %7.1f GB/s\n", bpc, ms * 1e3, gbs(ms, 1));
+        ms = time_kernel([&](int i) { k_fill<256, 4, 1><<<grid, 256>>>(P((i & 1) * 2 * bytes), n16, 7u); });
+        printf("write-only U=4 bpc=%2d     %8.1f us  %7.1f GB/s\n", bpc, ms * 1e3, gbs(ms, 1));
+    }
+    // copy: src at 0 / 2*bytes alternating, dst = src + bytes + delta
+    for (uint64_t delta : {0ull, 4096ull, 65536ull, 1ull << 20, (1ull << 20) + 4096, 3ull << 20, 7ull << 20,
+                           (32ull << 20) + 256}) {
+        for (int bpc : {8, 32}) {
+            const int grid = cus * bpc;
+            double ms = time_kernel([&](int i) {
+                const uint64_t s = (i & 1) * 2 * bytes;
+                k_stream<256, 4, 3><<<grid, 256>>>(P(s), P(s + bytes + delta), n16, 9u);
+            });
+            printf("copy delta=%9llu bpc=%2d  %8.1f us  %7.1f GB/s\n", (unsigned long long)delta, bpc, ms * 1e3,
+                   gbs(ms, 2));
+        }
+    }
+    for (int bpc : {4, 8, 16, 32}) {
+        const int grid = cus * bpc;
+        double ms = time_kernel([&](int i) {
+            const uint64_t s = (i & 1) * 2 * bytes;
+            k_stream<256, 4, 3><<<grid, 256>>>(P(s), P(s), n16, 9u);
+        });
+        printf("inplace bpc=%2d              %8.1f us  %7.1f GB/s\n", bpc, ms * 1e3, gbs(ms, 2));
+        ms = time_kernel([&](int i) {
+            const uint64_t s = (i & 1) * 2 * bytes;
+            k_pipe<4><<<grid, 256>>>(P(s), P(s + bytes), n16, 9u);
+        });
+        printf("pipelined U=4 bpc=%2d        %8.1f us  %7.1f GB/s\n", bpc, ms * 1e3, gbs(ms, 2));
+        ms = time_kernel([&](int i) {
+            const uint64_t s = (i & 1) * 2 * bytes;
+            k_pipe<2><<<grid, 256>>>(P(s), P(s + bytes), n16, 9u);
+        });
+        printf("pipelined U=2 bpc=%2d        %8.1f us  %7.1f GB/s\n", bpc, ms * 1e3, gbs(ms, 2));
+    }
+    {
+        double ms = time_kernel([&](int i) {
+            const uint64_t s = (i & 1) * 2 * bytes;
+            CK(hipMemcpyAsync(P(s + bytes), P(s), bytes, hipMemcpyDeviceToDevice));
+        });
+        printf("hipMemcpyDtoD               %8.1f us  %7.1f GB/s\n", ms * 1e3, gbs(ms, 2));
+    }
+    CK(hipFree(base));
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
     const uint64_t mib = argc > 1 ? strtoull(argv[1], 0, 10) : 256;
@@ -239,6 +374,8 @@ int main(int argc, char** argv)
     CK(hipGetDeviceProperties(&p, 0));
     const int cus = p.multiProcessorCount;
     printf("device %s CUs=%d bytes=%llu MiB\n", p.gcnArchName, cus, (unsigned long long)mib);
+    if (argc > 2 && std::string(argv[2]) == "explore")
+        return explore(bytes, cus);
     u32x4 *src, *dst;
     CK(hipMalloc(&src, bytes));
     CK(hipMalloc(&dst, bytes));

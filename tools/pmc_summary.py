@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--calib-bytes", type=float, default=float(1 << 30))
     ap.add_argument("--out")
     ap.add_argument("--config", default="c2")
-    ap.add_argument("--kernel", default="k_decode_unmask")
+    ap.add_argument("--kernel", default="k_decode")
     ap.add_argument("--alg-bytes", type=float, default=None)
     a = ap.parse_args()
     fetch, nf = load(a.fetch_dir, "FETCH_SIZE")

@@ -23,10 +23,24 @@ def main():
     # ROT distinct batches, used in turn, so no step finds its input in the
     # 256 MiB Infinity Cache left warm by the previous step
     rot = int(os.environ.get("ROT", 1))
-    wire, fs, _ = wl.c2_wire(n, size, seed=1)
-    ws = [torch.from_numpy(wire).cuda()] + [torch.from_numpy(wl.c2_wire(n, size, seed=2 + r)[0]).cuda()
-                                           for r in range(rot - 1)]
-    f = torch.from_numpy(fs.view(np.int64)).cuda()
+    ragged = os.environ.get("RAGGED")   # "lo,hi": C3-style ragged frames (payload uniform in [lo, hi])
+    if ragged:
+        lo, hi = (int(x) for x in ragged.split(","))
+        rot = 1   # a ragged batch (GBs) is far larger than the Infinity Cache anyway
+        enc = ca.Codec(0)
+        payload, desc = wl.c3_batch(n, lo, hi, seed=3)
+        w_, off = enc.encode_batch(torch.from_numpy(payload).cuda(), ca.desc_to_tensor(desc, "cuda"),
+                                   wire_cap=int(ca.frame_sizes(desc).sum()))
+        enc.sync()
+        enc.close()
+        ws, f = [w_], off[:-1].clone()
+        wire = ws[0].cpu().numpy()
+        size = len(wire) // n
+    else:
+        wire, fs, _ = wl.c2_wire(n, size, seed=1)
+        ws = [torch.from_numpy(wire).cuda()] + [torch.from_numpy(wl.c2_wire(n, size, seed=2 + r)[0]).cuda()
+                                               for r in range(rot - 1)]
+        f = torch.from_numpy(fs.view(np.int64)).cuda()
     outs = [torch.empty_like(ws[0]) for _ in range(rot)]
     info = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
     it = [0]
