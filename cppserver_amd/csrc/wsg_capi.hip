@@ -438,7 +438,7 @@ int wsg_fanout_encode(wsg_ctx* c, const uint8_t* d_payload, uint64_t len, const 
         return WSG_ENOMEM;
     hipStream_t s = pick(c, stream);
     const int t = timing_begin(c, s);
-    const uint64_t pieces = uint64_t(k) * ((fsize + 15 + wsg::PIECE - 1) / wsg::PIECE);
+    const uint64_t pieces = uint64_t(k) * ((fsize + wsg::PIECE_ALIGN - 1 + wsg::PIECE - 1) / wsg::PIECE);
     const uint64_t blocks = wsg::fanout_flat ? ceil_div(ceil_div(total, wsg::CHUNK), wsg::BLOCK * wsg::FAN_UNITS)
                                              : ceil_div(pieces, wsg::BLOCK / 64);
     WSG_HIP(wsg::launch_fanout(s, grid_for(c, blocks), d_payload, len, d_keys, k, opcode, mask ? 1u : 0u, fsize,

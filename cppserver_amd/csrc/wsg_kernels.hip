@@ -602,7 +602,8 @@ __global__ __launch_bounds__(BLOCK) void k_decode(const uint8_t* __restrict__ wi
 //
 // A piece is at most PIECE = 4 KiB of ONE frame's wire bytes, cut at absolute
 // 16-byte chunk boundaries: piece k of frame i covers
-//     [max(off_i, A_i + k*PIECE), min(end_i, A_i + (k+1)*PIECE)),   A_i = off_i & ~15.
+//     [max(off_i, A_i + k*PIECE), min(end_i, A_i + (k+1)*PIECE)),   A_i = off_i & ~127
+// (line-aligned output rows).
 // One wave encodes one piece, so the key, the key phase and the source shift
 // are uniform over it: full data chunks stream (aligned 16-B loads,
 // v_alignbyte_b32 funnel, XOR, 16-B nontemporal store).  Chunks holding
@@ -747,7 +748,7 @@ struct Piece {
     {
         R = rec;
         const uint32_t lane = threadIdx.x & 63;
-        lo = (R.off & ~uint64_t(15)) + k * PIECE;
+        lo = (R.off & ~(PIECE_ALIGN - 1)) + k * PIECE;
         live = exists && lo < R.end;   // piece counts are an upper bound
         hi = min(lo + PIECE, R.end);
         sbase = reinterpret_cast<uintptr_t>(R.src) - R.data_w;
@@ -787,7 +788,10 @@ struct Piece {
     }
 };
 
-__device__ __forceinline__ uint64_t pieces_of(uint64_t frame_bytes) { return (frame_bytes + 15 + PIECE - 1) / PIECE; }
+__device__ __forceinline__ uint64_t pieces_of(uint64_t frame_bytes)
+{
+    return (frame_bytes + PIECE_ALIGN - 1 + PIECE - 1) / PIECE;
+}
 
 } // namespace
 

@@ -324,8 +324,8 @@ static int explore(uint64_t bytes, int cus)
         printf("write-only U=4 bpc=%2d     %8.1f us  %7.1f GB/s\n", bpc, ms * 1e3, gbs(ms, 1));
     }
     // copy: src at 0 / 2*bytes alternating, dst = src + bytes + delta
-    for (uint64_t delta : {0ull, 4096ull, 65536ull, 1ull << 20, (1ull << 20) + 4096, 3ull << 20, 7ull << 20,
-                           (32ull << 20) + 256}) {
+    for (uint64_t delta : {0ull, 16ull, 80ull, 4096ull, 65536ull, 1ull << 20, (1ull << 20) + 4096, 3ull << 20,
+                           7ull << 20, (32ull << 20) + 256}) {
         for (int bpc : {8, 32}) {
             const int grid = cus * bpc;
             double ms = time_kernel([&](int i) {
