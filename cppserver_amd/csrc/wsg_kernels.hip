@@ -51,7 +51,10 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #define WSG_DIAG 0   // 5: timing-only diagnostic build of k_decode (every tile streams; tools/)
 #endif
 #ifndef WSG_DIAG_FAN
-#define WSG_DIAG_FAN 0   // timing-only fan-out diagnostics: 1 no key loads, 2 no payload loads, 4 stores only
+#define WSG_DIAG_FAN 0   // timing-only fan-out diagnostics: 1 no key loads, 2 no payload loads, 4 stores only, 8 no edge blocks
+#endif
+#ifndef WSG_DEC_WAVES
+#define WSG_DEC_WAVES 1   // k_decode minimum waves/SIMD (register cap); 6 and 8 spill and run slower
 #endif
 #ifndef WSG_NT_STORE
 #define WSG_NT_STORE 1
@@ -423,7 +426,7 @@ __device__ __forceinline__ v4u seg_xor(uint32_t o, const Seg& s)
 
 // Decode (ws.cpp:320-406 over a batch): out = wire with every payload XORed
 // by its key; info[i] and the error latch per frame.
-__global__ __launch_bounds__(BLOCK) void k_decode(const uint8_t* __restrict__ wire, uint8_t* out, uint64_t wire_len,
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_WAVES))) void k_decode(const uint8_t* __restrict__ wire, uint8_t* out, uint64_t wire_len,
                                                   const uint64_t* __restrict__ fs, uint32_t n, double frames_per_byte,
                                                   uint32_t stride, wsg_recv_info* __restrict__ info,
                                                   unsigned long long* err, uint64_t num_tiles)
@@ -477,8 +480,9 @@ __global__ __launch_bounds__(BLOCK) void k_decode(const uint8_t* __restrict__ wi
                 c = k + 1;
         }
 
-        if (WSG_DIAG == 5 || c <= MAXF) {
-            // frames' payload segments in scalar registers
+        if (WSG_DIAG == 5 || (full && c <= MAXF)) {
+            // frames' payload segments in scalar registers (full tiles; the
+            // wire's last, partial tile takes the staged path)
             Seg S[MAXF];
 #pragma unroll
             for (int k = 0; k < MAXF; ++k) {
@@ -494,7 +498,7 @@ __global__ __launch_bounds__(BLOCK) void k_decode(const uint8_t* __restrict__ wi
 #if WSG_DIAG == 5   // timing-only: every tile streams with its first frame's key (8-wave register budget)
             if (true) {
 #else
-            if (full && S[0].lo == 0 && S[0].hi == TILE) {
+            if (S[0].lo == 0 && S[0].hi == TILE) {
 #endif
                 // stream: the whole tile is payload of one frame
 #pragma unroll
@@ -521,7 +525,7 @@ __global__ __launch_bounds__(BLOCK) void k_decode(const uint8_t* __restrict__ wi
                     for (int k = 1; k < MAXF; ++k)
                         x |= seg_xor(o, S[k]);
                 }
-                store_chunk(out, base + o, tend, v[u] ^ x);
+                st16nt(out + base + o, v[u] ^ x);
             }
             continue;
         }
@@ -569,29 +573,49 @@ __global__ __launch_bounds__(BLOCK) void k_decode(const uint8_t* __restrict__ wi
                 x |= seg_xor(o, Seg{s_lo[j], s_hi[j], s_kr[j]});
             return x;
         };
-        int cnt;
-        bool more;
-        stage(L.first, cnt, more);
-        if (!more) {
+        // rounds of LDSF frames; one round (the common case) stores straight
+        // from registers, more rounds (tiny frames) accumulate each thread's
+        // XOR words in its own LDS slots (a register array carried around
+        // the round loop would cost occupancy)
+        __shared__ v4u s_acc[UNROLL][BLOCK];
+        for (uint64_t r0 = L.first;; r0 += LDSF) {
+            int cnt;
+            bool more;
+            stage(r0, cnt, more);
+            if (r0 == L.first && !more) {
+                // whole chunks stored as they are built; the one chunk the
+                // wire's end cuts (if any) afterwards: one byte loop
+                v4u tail_w = {0, 0, 0, 0};
+                uint64_t tail_p = ~uint64_t(0);
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
-                store_chunk(out, base + lane_off(u), tend, v[u] ^ chunk_xor(uint32_t(lane_off(u)), cnt));
-            continue;
-        }
-        // more than LDSF frames touch the tile (tiny frames): chunk by chunk,
-        // every round restaged, the data re-read
-#pragma unroll 1
-        for (int u = 0; u < UNROLL; ++u) {
-            const uint32_t o = uint32_t(lane_off(u));
-            v4u x = {0, 0, 0, 0};
-            for (uint64_t r0 = L.first;; r0 += LDSF) {
-                stage(r0, cnt, more);
-                x |= chunk_xor(o, cnt);
-                if (!more)
-                    break;
+                for (int u = 0; u < UNROLL; ++u) {
+                    const uint64_t p = base + lane_off(u);
+                    const v4u w = v[u] ^ chunk_xor(uint32_t(lane_off(u)), cnt);
+                    if (p + CHUNK <= tend) {
+                        st16nt(out + p, w);
+                    } else if (p < tend) {
+                        tail_w = w;
+                        tail_p = p;
+                    }
+                }
+                if (tail_p != ~uint64_t(0))
+                    store_partial(out + tail_p, tail_w, uint32_t(tend - tail_p));
+                break;
             }
-            const v4u d = o < span ? ld16(wire + base + o) : v4u{0, 0, 0, 0};
-            store_chunk(out, base + o, tend, d ^ x);
+#pragma unroll 1
+            for (int u = 0; u < UNROLL; ++u) {
+                const v4u x = chunk_xor(uint32_t(lane_off(u)), cnt);
+                s_acc[u][threadIdx.x] = (r0 == L.first) ? x : (s_acc[u][threadIdx.x] | x);
+            }
+            if (more)
+                continue;
+#pragma unroll 1
+            for (int u = 0; u < UNROLL; ++u) {
+                const uint64_t p = base + lane_off(u);
+                const v4u d = p < tend ? ld16(wire + p) : v4u{0, 0, 0, 0};
+                store_chunk(out, p, tend, d ^ s_acc[u][threadIdx.x]);
+            }
+            break;
         }
     }
 }
@@ -1117,7 +1141,7 @@ __global__ __launch_bounds__(BLOCK) void k_fanout_flat(const uint8_t* __restrict
         // edge items: 2 per frame start (the last "start" is the wire's end)
         const uint64_t item = uint64_t(blockIdx.x) * BLOCK + threadIdx.x;
         const uint64_t fr = item >> 1, h = item & 1;
-        if (fr > k)
+        if (fr > k || (WSG_DIAG_FAN & 8))
             return;
         const uint64_t start = fr * fsize;
         const uint64_t c = start / CHUNK + h;
