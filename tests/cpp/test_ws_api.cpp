@@ -8,6 +8,9 @@
 #include "server/ws/ws_handshake.h"
 #include "server/ws/ws_server.h"
 #include "server/ws/ws_session.h"
+#include "server/ws/wss_client.h"
+#include "server/ws/wss_server.h"
+#include "server/ws/wss_session.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -407,6 +410,87 @@ static void test_batched_send()
     server.EnableBatchSend(false);
 }
 
+// WSS (reference include/server/ws/wss_*.h): the same codec over a transport
+// that transforms the byte stream (a toy stream cipher standing in for TLS
+// records).  The WebSocket layer must not see the difference.
+struct ToyTls : Loopback {
+    uint8_t k_out = 0x5A, k_in = 0x5A;
+    size_t Send(const void* b, size_t n) override
+    {
+        std::vector<uint8_t> c((const uint8_t*)b, (const uint8_t*)b + n);
+        for (auto& x : c)
+            x ^= k_out++;   // "encrypt"
+        return Loopback::Send(c.data(), c.size());
+    }
+    // the peer's records, decrypted before they reach the WebSocket layer
+    std::vector<uint8_t> take()
+    {
+        std::vector<uint8_t> p(inbox.begin(), inbox.end());
+        inbox.clear();
+        for (auto& x : p)
+            x ^= k_in++;
+        return p;
+    }
+};
+
+struct TlsClient : WSSClient {
+    using WSSClient::WSSClient;
+    std::vector<std::vector<uint8_t>> messages;
+    void onWSConnecting(CppServer::HTTP::HTTPRequest& request) override
+    {
+        request.SetBegin("GET", "/");
+        request.SetHeader("Host", "localhost");
+        request.SetHeader("Upgrade", "websocket");
+        request.SetHeader("Connection", "Upgrade");
+        request.SetHeader("Sec-WebSocket-Key", Base64Encode(ws_nonce()));
+        request.SetHeader("Sec-WebSocket-Version", "13");
+    }
+    void onWSReceived(const void* b, size_t n) override { messages.emplace_back((const uint8_t*)b, (const uint8_t*)b + n); }
+};
+
+struct TlsSession : WSSSession {
+    using WSSSession::WSSSession;
+    void onWSReceived(const void* b, size_t n) override { SendBinaryAsync(b, n); }
+};
+
+static void test_wss()
+{
+    ToyTls ct, st;
+    ct.peer = &st;
+    st.peer = &ct;
+    TlsClient client(ct);
+    auto session = std::make_shared<TlsSession>(st);
+    WSSServer server;
+    server.AddSession(session);
+    auto pump = [&] {
+        for (int guard = 0; guard < 100 && (!ct.inbox.empty() || !st.inbox.empty()); ++guard) {
+            if (!st.inbox.empty()) {
+                auto b = st.take();
+                session->onReceived(b.data(), b.size());
+            }
+            if (!ct.inbox.empty()) {
+                auto b = ct.take();
+                client.onReceived(b.data(), b.size());
+            }
+        }
+    };
+    session->Connect();
+    client.Connect();
+    pump();
+    CHECK(client.IsConnected());
+    std::vector<uint8_t> big(70000);
+    for (size_t i = 0; i < big.size(); ++i)
+        big[i] = uint8_t(i * 7 + 1);
+    CHECK(client.SendBinaryAsync(big.data(), big.size()));
+    CHECK(client.SendTextAsync("over tls"));
+    pump();
+    CHECK(client.messages.size() == 2 && client.messages[0] == big &&
+          std::string(client.messages[1].begin(), client.messages[1].end()) == "over tls");
+    CHECK(server.MulticastText("all") > 0);
+    pump();
+    CHECK(client.messages.size() == 3 && std::string(client.messages[2].begin(), client.messages[2].end()) == "all");
+}
+
 int main()
 {
     try {
@@ -417,6 +501,7 @@ int main()
         test_soak();
         test_batched_server_receive();
         test_batched_send();
+        test_wss();
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());
         return 2;
