@@ -291,6 +291,26 @@ def test_fanout_tiny_unaligned_tail(codec, length, k, opcode, mask, src_off):
     assert (got[len(ref):] == 0xA5).all()
 
 
+@pytest.mark.parametrize("length,k,opcode,mask,src_off", [(1010, 700, 0x82, True, 0), (1018, 333, 0x89, False, 3),
+                                                         (2047, 64, 0x8A, True, 1), (4096, 4097, 0x82, False, 0),
+                                                         (4100, 999, 0x81, True, 11), (8190, 130, 0x89, True, 8),
+                                                         (12268, 33, 0x82, True, 2), (12290, 7, 0x82, True, 0)])
+def test_fanout_mid_sizes(codec, length, k, opcode, mask, src_off):
+    """Frames of 1-12 KiB: frame starts at every phase of the 16-B chunks,
+    status-prefixed opcodes, unmasked frames still XORed (Q1),
+    unaligned payload sources, nothing written past the last frame."""
+    payload, keys = wl.c4_fanout(length, k, seed=3 * length + k)
+    ref = oracle.fanout_encode(payload, keys, opcode, mask)
+    buf = np.zeros(length + src_off + 1, np.uint8)
+    buf[src_off: src_off + length] = payload
+    wire = torch.full((len(ref) + 48,), 0xA5, dtype=torch.uint8, device="cuda")
+    codec.fanout(dev(buf)[src_off:], dev(keys.view(np.int32)), opcode, mask, wire=wire, length=length)
+    codec.sync()
+    got = wire.cpu().numpy()
+    assert np.array_equal(got[: len(ref)], ref)
+    assert (got[len(ref):] == 0xA5).all()
+
+
 # ---------------------------------------------------------------- edge cases
 def test_empty_batches(codec):
     rc, out, info = gpu_decode(codec, np.zeros(32, np.uint8), [])

@@ -1,6 +1,7 @@
 """Interleaved A/B timing of encode variants (libwsg.so builds) on C5/C3-like batches.
 
-usage: CFG=c5|c3 python tools/tune_enc.py path/to/libwsg.so ...
+usage: CFG=c5|c3|c4 python tools/tune_enc.py [NAME=VALUE@]path/to/libwsg.so ...
+(NAME=VALUE is set in the environment before that library's context is made)
 """
 import os
 import statistics
@@ -12,6 +13,14 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import cppserver_amd as ca  # noqa: E402
 from cppserver_amd import workloads as wl  # noqa: E402
+
+
+def make_codec(spec):
+    if spec and "@" in spec:
+        env, _, spec = spec.partition("@")
+        name, _, value = env.partition("=")
+        os.environ[name] = value
+    return ca.Codec(0, lib_path=spec or None)
 
 
 def main():
@@ -30,7 +39,7 @@ def main():
     d = ca.desc_to_tensor(desc, "cuda")
     wires = [torch.empty(cap, dtype=torch.uint8, device="cuda") for _ in range(2)]
     woff = torch.empty(n + 1, dtype=torch.int64, device="cuda")
-    codecs = [ca.Codec(0, lib_path=l) for l in libs]
+    codecs = [make_codec(l) for l in libs]
     kern = [[] for _ in libs]
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for rep in range(int(os.environ.get("REPS", 5))):
@@ -57,7 +66,7 @@ def fanout(libs):
     p = torch.from_numpy(payload).cuda()
     kt = torch.from_numpy(keys.view(np.int32)).cuda()
     wires = [torch.empty(fsz * len(keys), dtype=torch.uint8, device="cuda") for _ in range(2)]
-    codecs = [ca.Codec(0, lib_path=l) for l in libs]
+    codecs = [make_codec(l) for l in libs]
     kern = [[] for _ in libs]
     for rep in range(int(os.environ.get("REPS", 5))):
         for ci, c in enumerate(codecs):
