@@ -336,6 +336,29 @@ def test_decode_errors_match_oracle(codec):
         assert np.array_equal(out_g, out_o)
 
 
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_decode_garbage_starts_match_oracle(codec, seed):
+    """Frame-start tables that break the contract (unsorted, repeated, past
+    the wire's end, pointing into payloads): the launch ends, the status and
+    every frame's error code are the oracle's (output bytes are unspecified
+    for such a batch)."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 3000, 300).astype(np.uint64)
+    wire, fs = _frames_wire(rng, lens)
+    bad = fs.copy()
+    pick = rng.random(len(bad))
+    bad[pick < 0.2] = rng.integers(0, len(wire) + 100, int((pick < 0.2).sum()))
+    bad[(pick >= 0.2) & (pick < 0.25)] = 0
+    rng.shuffle(bad[: len(bad) // 3])
+    rc_o, _, info_o = oracle.decode_batch(wire, bad)
+    rc_g, _, info_g = gpu_decode(codec, wire, bad)
+    assert rc_o != 0 and rc_g == rc_o
+    assert np.array_equal(info_g["error"], info_o["error"])
+    ok = info_o["error"] == 0
+    for f in INFO_FIELDS:
+        assert np.array_equal(info_g[f][ok], info_o[f][ok]), f
+
+
 def test_misaligned_buffers_rejected(codec):
     w = torch.zeros(64, dtype=torch.uint8, device="cuda")
     f = torch.zeros(1, dtype=torch.int64, device="cuda")
