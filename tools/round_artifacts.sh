@@ -8,7 +8,7 @@ R=${ROUND:-r1}
 OUT=gpurun_out/art_$R
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="python bench.py --steps ${STEPS:-40} --warmup 3"
+B="python bench.py ${STEPS:+--steps $STEPS}"   # bench.py defaults unless STEPS is set
 echo "== bench"
 timeout -k 10 600 $B > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
 tail -1 "$OUT/bench.json"
