@@ -26,6 +26,7 @@ struct wsg_ctx {
     hipStream_t stream = nullptr;
     int num_cus = 256;
     int blocks_per_cu = 32;   // measured best for the C2 unmask (tools/tune.py)
+    uint64_t small_avg = wsg::SMALL_AVG;   // batch encode: k_encode_small when wire_cap <= n * small_avg
     unsigned long long* d_err = nullptr;
     // scratch
     wsg_enc_scratch enc;
@@ -260,6 +261,8 @@ int wsg_create(int device, wsg_ctx** out)
         if (v > 0 && v <= 256)
             c->blocks_per_cu = v;
     }
+    if (const char* e = std::getenv("WSG_SMALL_AVG"))   // A/B measurements (tools/tune_enc.py)
+        c->small_avg = std::strtoull(e, nullptr, 10);
     *out = c;
     return WSG_OK;
 }
@@ -398,8 +401,11 @@ int encode_launch(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, const wsg
     WSG_HIP(wsg::launch_encode_scan(s, d_desc, n, d_wire_off, e.d_piece_start, e.d_scan, e.d_piece_frame, pieces_cap,
                                     wire_cap, c->d_err));
     const int t = timing_begin(c, s);
-    WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, ceil_div(pieces_cap, wsg::BLOCK / 64)), d_payload, d_desc, n,
-                                    d_wire_off, e.d_piece_start, e.d_piece_frame, d_wire, wire_cap));
+    if (wire_cap <= uint64_t(n) * c->small_avg)   // small frames: one block per group of frames
+        WSG_HIP(wsg::launch_encode_small(s, d_payload, d_desc, n, d_wire_off, d_wire, wire_cap));
+    else
+        WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, ceil_div(pieces_cap, wsg::BLOCK / 64)), d_payload, d_desc, n,
+                                        d_wire_off, e.d_piece_start, e.d_piece_frame, d_wire, wire_cap));
     timing_end(c, s, t);
     return WSG_OK;
 }

@@ -27,6 +27,18 @@ constexpr bool fanout_flat = WSG_FANOUT_FLAT != 0;       // fan-out: flat chunk 
 #define WSG_FAN_UNITS 4
 #endif
 constexpr int FAN_UNITS = WSG_FAN_UNITS;                 // fan-out: 16-B chunks per lane per pass
+#ifndef WSG_SMALL_FPT
+#define WSG_SMALL_FPT 1
+#endif
+constexpr uint32_t SMALL_F = BLOCK * WSG_SMALL_FPT;       // small-frame encode: frames per block
+#ifndef WSG_SMALL_AVG
+#define WSG_SMALL_AVG 4096
+#endif
+constexpr uint64_t SMALL_AVG = WSG_SMALL_AVG;            // ... used when wire_cap <= n * SMALL_AVG
+#ifndef WSG_SMALL_RANGE
+#define WSG_SMALL_RANGE 32768
+#endif
+constexpr uint64_t SMALL_RANGE = WSG_SMALL_RANGE;        // ... wire bytes per block (sets frames per block)
 constexpr int SCAN_PER_LANE = 4;
 constexpr uint64_t SCAN_ITEMS = uint64_t(BLOCK) * SCAN_PER_LANE;   // frames per scan block
 
@@ -48,6 +60,9 @@ hipError_t launch_encode_scan(hipStream_t s, const wsg_send_desc* desc, uint32_t
 hipError_t launch_encode_mask(hipStream_t s, int grid, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
                               const uint64_t* wire_off, const uint32_t* piece_start, const uint32_t* piece_frame,
                               uint8_t* wire, uint64_t wire_cap);
+// Batch encode with one block per SMALL_F consecutive frames (after the scan).
+hipError_t launch_encode_small(hipStream_t s, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
+                               const uint64_t* wire_off, uint8_t* wire, uint64_t wire_cap);
 hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64_t len, const uint32_t* keys,
                          uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire);
 hipError_t launch_xor(hipStream_t s, int grid, const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,

@@ -1085,6 +1085,105 @@ __device__ __forceinline__ v4u fan_frame_bytes(const uint8_t* __restrict__ paylo
     return out;
 }
 
+// ---- batch encode of small frames -----------------------------------------
+// The piece kernel spends one wave pass per frame whatever its size, so a
+// batch of frames a few dozen bytes long (the reference's 32-byte echo
+// messages) leaves most lanes idle.  Here a block owns fpb <= SMALL_F
+// consecutive frames (about SMALL_RANGE wire bytes at the batch's average
+// frame size), i.e. one contiguous wire range, and its lanes own the 16-B chunks
+// of that range.  A chunk is ORed together from the frames it overlaps: each
+// frame's head (header + close-status bytes, <= 16, built once per frame into
+// LDS) shifted into place, plus its masked payload window.  The chunks at the
+// two ends of the range, shared with the neighbouring blocks, get byte stores
+// of this block's bytes only.  Correct for any sizes; the host picks it when
+// the average frame is small (SMALL_AVG).
+struct SmallFrame {
+    uint64_t src;   // address of the first data byte
+    uint32_t key;
+    uint32_t geo;   // head bytes (header + status) | header bytes << 8
+};
+
+// Bytes [o, o + 16) of a frame of fsize bytes (o < fsize), 0 past its end.
+__device__ __forceinline__ v4u small_bytes(v4u head, const SmallFrame& f, uint64_t fsize, uint64_t o)
+{
+    const uint32_t data0 = f.geo & 0xFFu, hdr = f.geo >> 8;
+    v4u out = shr_bytes(head, o);
+    const uint64_t lo = o < data0 ? data0 - o : 0;   // chunk bytes [lo, hi) are payload
+    const uint64_t hi = fsize - o < CHUNK ? fsize - o : CHUNK;
+    if (lo < hi) {
+        const v4u w = fan_window(reinterpret_cast<const uint8_t*>(f.src), fsize - data0, int64_t(o) - int64_t(data0));
+        out |= (w ^ key_rot(f.key, uint32_t(o - hdr))) & (low_bytes(hi) & ~low_bytes(lo));
+    }
+    return out;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_encode_small(const uint8_t* __restrict__ payload,
+                                                        const wsg_send_desc* __restrict__ desc, uint32_t n,
+                                                        uint32_t fpb, const uint64_t* __restrict__ wire_off,
+                                                        uint8_t* __restrict__ wire, uint64_t wire_cap)
+{
+    __shared__ uint64_t s_off[SMALL_F + 1];
+    __shared__ v4u s_head[SMALL_F];
+    __shared__ SmallFrame s_fr[SMALL_F];
+    if (wire_off[n] > wire_cap)
+        return;   // capacity error latched by k_encode_finalize
+    const uint32_t f_lo = blockIdx.x * fpb;   // fpb <= SMALL_F (host)
+    if (f_lo >= n)
+        return;
+    const uint32_t cnt = min(n - f_lo, fpb);
+    for (uint32_t t = threadIdx.x; t < cnt; t += BLOCK) {
+        const uint32_t i = f_lo + t;
+        const Desc d = load_desc(desc + i);
+        const SendGeom g = send_geom(d.opcode, d.mask, d.len, d.status);
+        v4u h = {0, 0, 0, 0};
+#pragma unroll 1
+        for (uint32_t r = 0; r < g.hdr; ++r)
+            put_byte(h, r, header_byte(d.opcode, d.mask, g.body, d.key, r));
+        if (g.prefix) {   // close status, big-endian, masked like payload bytes 0-1
+            put_byte(h, g.hdr, uint32_t((d.status >> 8) & 0xFF) ^ key_byte(d.key, 0));
+            put_byte(h, g.hdr + 1, uint32_t(d.status & 0xFF) ^ key_byte(d.key, 1));
+        }
+        s_head[t] = h;
+        s_fr[t] = SmallFrame{reinterpret_cast<uintptr_t>(payload + d.src_off), d.key,
+                             (g.hdr + g.prefix) | (g.hdr << 8)};
+        s_off[t] = wire_off[i];
+    }
+    if (threadIdx.x == 0)
+        s_off[cnt] = wire_off[f_lo + cnt];
+    __syncthreads();
+    const uint64_t r_lo = s_off[0], r_hi = s_off[cnt];
+    for (uint64_t p = (r_lo & ~uint64_t(CHUNK - 1)) + uint64_t(threadIdx.x) * CHUNK; p < r_hi;
+         p += uint64_t(BLOCK) * CHUNK) {
+        uint32_t a = 0, b = cnt - 1;   // last frame starting at or before p (frame 0 before the range)
+        while (a < b) {
+            const uint32_t m = (a + b + 1) >> 1;
+            if (s_off[m] <= p)
+                a = m;
+            else
+                b = m - 1;
+        }
+        v4u w = {0, 0, 0, 0};
+        for (uint32_t j = a; j < cnt; ++j) {
+            const uint64_t off = s_off[j];
+            if (off >= p + CHUNK)
+                break;
+            const uint64_t fsize = s_off[j + 1] - off;
+            if (p >= off)
+                w |= small_bytes(s_head[j], s_fr[j], fsize, p - off);
+            else
+                w |= shl_bytes(small_bytes(s_head[j], s_fr[j], fsize, 0), off - p);
+        }
+        if (p >= r_lo && p + CHUNK <= r_hi) {
+            st16nt(wire + p, w);
+        } else {
+            const uint32_t j0 = p < r_lo ? uint32_t(r_lo - p) : 0;
+            const uint32_t j1 = r_hi - p < CHUNK ? uint32_t(r_hi - p) : CHUNK;
+            for (uint32_t j = j0; j < j1; ++j)
+                wire[p + j] = uint8_t(lane_byte(w, j));
+        }
+    }
+}
+
 // Grid = `main_blocks` streaming blocks, then the edge blocks.
 //  * Streaming waves own 64 x FU consecutive chunks and write every chunk
 //    that is all payload of one frame (the frame index comes from one scalar
@@ -1281,6 +1380,19 @@ hipError_t launch_encode_mask(hipStream_t s, int grid, const uint8_t* payload, c
                               uint8_t* wire, uint64_t wire_cap)
 {
     k_encode_mask<<<grid, BLOCK, 0, s>>>(payload, desc, n, wire_off, piece_start, piece_frame, wire, wire_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_small(hipStream_t s, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
+                               const uint64_t* wire_off, uint8_t* wire, uint64_t wire_cap)
+{
+    // frames per block: as many as fit SMALL_RANGE wire bytes at the average
+    // frame size (wire_cap / n), so that larger frames still fill the grid
+    const uint64_t avg = wire_cap / n + 1;
+    uint32_t fpb = SMALL_F;
+    while (fpb > 1 && uint64_t(fpb) * avg > SMALL_RANGE)
+        fpb >>= 1;
+    k_encode_small<<<(n + fpb - 1) / fpb, BLOCK, 0, s>>>(payload, desc, n, fpb, wire_off, wire, wire_cap);
     return hipGetLastError();
 }
 

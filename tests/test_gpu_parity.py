@@ -165,6 +165,51 @@ def test_encode_mixed_vs_oracle(codec, lo, hi, n):
     assert_decode_parity(codec, wire_o, off_o[:-1])
 
 
+SMALL_AVG = 4096   # wsg_internal.h: the small-frame kernel runs when wire_cap <= n * SMALL_AVG
+
+
+@pytest.mark.parametrize("case", ["tiny", "one", "block-edge", "big-among-small", "close-status", "len-classes",
+                                  "mid"])
+def test_encode_small_and_piece_kernels(codec, case):
+    """Both batch-encode kernels on the same frames: k_encode_small (exact
+    capacity, average frame <= SMALL_AVG) and the piece kernel (capacity
+    raised past n * SMALL_AVG), each byte-identical to the oracle."""
+    rng = np.random.default_rng(sum(map(ord, case)) + 5)
+    if case == "tiny":
+        payload, desc = _mixed_desc(rng, 3000, 0, 40)
+    elif case == "one":
+        payload, desc = _mixed_desc(rng, 1, 5, 5)
+    elif case == "block-edge":       # 256 frames per block at this size: the last block holds one
+        payload, desc = _mixed_desc(rng, 257, 0, 20)
+    elif case == "big-among-small":  # a block whose wire range spans many passes of its lanes
+        payload, desc = _mixed_desc(rng, 2000, 0, 64)
+        big = rng.choice(2000, 8, replace=False)
+        desc["len"][big] = rng.integers(60000, 100000, 8)
+        desc["src_off"] = rng.integers(0, 16, 2000).astype(np.uint64)
+        payload = wl.random_bytes(rng, 100016)
+    elif case == "mid":              # ~3 KiB average: 8 frames per block
+        payload, desc = _mixed_desc(rng, 1500, 0, 6000)
+    elif case == "close-status":
+        payload, desc = _mixed_desc(rng, 1500, 0, 30)
+        desc["opcode"] = 0x88
+        desc["status"] = rng.integers(-3, 70000, 1500)
+    else:                             # 7/16/64-bit length fields around their edges
+        payload, desc = _mixed_desc(rng, 3000, 0, 3)
+        desc["len"] = rng.choice([0, 1, 2, 15, 16, 17, 124, 125, 126, 127, 128], 3000)
+        desc["len"][rng.choice(3000, 6, replace=False)] = [65535, 65536, 65537, 65535, 65536, 70000]
+        desc["src_off"] = rng.integers(0, 16, 3000).astype(np.uint64)
+        payload = wl.random_bytes(rng, 70016)
+    n = len(desc)
+    wire_o, off_o = oracle.encode_batch(payload, desc)
+    exact = int(off_o[n])
+    assert exact <= n * SMALL_AVG
+    for cap in (exact, n * SMALL_AVG + 4096):
+        rc, wire_g, off_g = gpu_encode(codec, payload, desc, cap=cap)
+        assert rc == 0
+        assert np.array_equal(off_g, off_o), cap
+        assert np.array_equal(wire_g, wire_o), cap
+
+
 # ------------------------------------------- k_decode tile paths (one launch)
 def _frames_wire(rng, lens, gaps=None, lead=0):
     """Masked/unmasked frames of the given payload lengths back to back, with

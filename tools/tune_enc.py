@@ -30,9 +30,9 @@ def main():
         return fanout(libs)
     if cfg == "c5":
         payload, desc, _ = wl.c5_shard(0, 8, n_total=1 << 20)      # one rank's share of 8: 131072 x 16 KiB
-    else:
-        payload, desc = wl.c3_batch(16384, 128, 65536, seed=3)
-    cap = int(sum(ca.frame_size(int(d["opcode"]), bool(d["mask"]), int(d["len"])) for d in desc[:1])) * 0
+    else:   # $FRAMES frames, payload uniform in [$LO, $HI] (default: C3-like)
+        payload, desc = wl.c3_batch(int(os.environ.get("FRAMES", 16384)), int(os.environ.get("LO", 128)),
+                                    int(os.environ.get("HI", 65536)), seed=3)
     cap = int(np.sum([ca.frame_size(0x82, True, int(x)) for x in desc["len"]]))
     n = len(desc)
     p = [torch.from_numpy(payload).cuda() for _ in range(2)]
