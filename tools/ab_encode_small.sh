@@ -1,3 +1,7 @@
+#!/bin/bash
+# A/B of the batch-encode kernels on small/mid frame batches (GPU box):
+# default build, frames-per-block variants, and the piece kernel (WSG_SMALL_AVG=0).
+# Build the variants first: tools/build_variant.sh {pieces,f2 -DWSG_SMALL_FPT=2,f4 -DWSG_SMALL_FPT=4}
 mkdir -p gpurun_out/ab
 V=cppserver_amd/_build/var
 for spec in "1000000 32 32" "200000 0 1024" "100000 0 2048" "50000 0 4096" "1000000 0 64" "20000 0 8192"; do set -- $spec
