@@ -311,15 +311,20 @@ def session_batch_leg(timeout=240):
     if not os.path.exists(exe):
         return None
     out = {}
-    for mode, args in (("rx", ["1024", "4", "65536", "16384", "3"]), ("tx", ["1024", "4", "65536", "0", "3"])):
+    legs = (("rx", ["1024", "4", "65536", "16384", "3"]), ("tx", ["1024", "4", "65536", "0", "3"]),
+            # echo-sized messages (32 B payload): 256 sessions x 64 frames
+            ("rx_32B", ["256", "64", "32", "0", "3"]), ("tx_32B", ["256", "64", "32", "0", "3"]))
+    for leg, args in legs:
+        mode = leg.split("_")[0]
         r = subprocess.run([exe, mode] + args, capture_output=True, text=True, timeout=timeout)
         if r.returncode != 0:
-            out[mode] = {"error": (r.stderr or r.stdout).strip()[-300:]}
+            out[leg] = {"error": (r.stderr or r.stdout).strip()[-300:]}
             continue
         d = json.loads(r.stdout.strip().splitlines()[-1])
-        out[mode] = {k: d[k] for k in ("batched_GiBps", "per_call_GiBps", "batched_frames_per_s",
+        out[leg] = {k: d[k] for k in ("batched_GiBps", "per_call_GiBps", "batched_frames_per_s",
                                        "per_call_frames_per_s", "delivered_ok")}
-    out["workload"] = "1024 sessions x 4 frames x 64 KiB, host buffers (PCIe + host framing + callbacks inside)"
+    out["workload"] = ("rx/tx: 1024 sessions x 4 frames x 64 KiB; *_32B: 256 sessions x 64 frames x 32 B; "
+                       "host buffers (PCIe + host framing + callbacks inside)")
     return out
 
 
