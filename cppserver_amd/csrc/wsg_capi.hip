@@ -385,27 +385,39 @@ namespace {
 // upper bound of the pieces: sum of ceil((size + 15) / PIECE) over frames
 inline uint64_t pieces_bound(uint32_t n, uint64_t wire_cap) { return wire_cap / wsg::PIECE + 2 * uint64_t(n) + 1; }
 
-int ensure_enc(wsg_enc_scratch& e, uint32_t n, uint64_t wire_cap)
+// Small-frame batches (average frame <= small_avg) take k_encode_small,
+// the rest the piece kernel.
+bool small_path(const wsg_ctx* c, uint32_t n, uint64_t wire_cap) { return wire_cap <= uint64_t(n) * c->small_avg; }
+
+// scratch for either path (the piece map only for the piece kernel; for
+// both when c is null)
+int ensure_enc(const wsg_ctx* c, wsg_enc_scratch& e, uint32_t n, uint64_t wire_cap)
 {
     if (int rc = ensure_array(e.d_scan, e.scan_cap, 4 * ceil_div(n, wsg::SCAN_ITEMS)))
         return rc;
     if (int rc = ensure_array(e.d_piece_start, e.piece_start_cap, uint64_t(n) + 1))
         return rc;
+    if (c && small_path(c, n, wire_cap))
+        return WSG_OK;
     return ensure_array(e.d_piece_frame, e.piece_frame_cap, pieces_bound(n, wire_cap));
 }
 
 int encode_launch(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, const wsg_send_desc* d_desc, uint32_t n,
                   uint8_t* d_wire, uint64_t wire_cap, uint64_t* d_wire_off, wsg_enc_scratch& e)
 {
+    if (small_path(c, n, wire_cap)) {   // sizes scan, then one block per group of frames
+        WSG_HIP(wsg::launch_encode_scan_small(s, d_desc, n, d_wire_off, e.d_piece_start, e.d_scan));
+        const int t = timing_begin(c, s);
+        WSG_HIP(wsg::launch_encode_small(s, d_payload, d_desc, n, d_wire_off, e.d_scan, d_wire, wire_cap, c->d_err));
+        timing_end(c, s, t);
+        return WSG_OK;
+    }
     const uint64_t pieces_cap = pieces_bound(n, wire_cap);
     WSG_HIP(wsg::launch_encode_scan(s, d_desc, n, d_wire_off, e.d_piece_start, e.d_scan, e.d_piece_frame, pieces_cap,
                                     wire_cap, c->d_err));
     const int t = timing_begin(c, s);
-    if (wire_cap <= uint64_t(n) * c->small_avg)   // small frames: one block per group of frames
-        WSG_HIP(wsg::launch_encode_small(s, d_payload, d_desc, n, d_wire_off, d_wire, wire_cap));
-    else
-        WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, ceil_div(pieces_cap, wsg::BLOCK / 64)), d_payload, d_desc, n,
-                                        d_wire_off, e.d_piece_start, e.d_piece_frame, d_wire, wire_cap));
+    WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, ceil_div(pieces_cap, wsg::BLOCK / 64)), d_payload, d_desc, n,
+                                    d_wire_off, e.d_piece_start, e.d_piece_frame, d_wire, wire_cap));
     timing_end(c, s, t);
     return WSG_OK;
 }
@@ -424,7 +436,7 @@ int wsg_encode_batch(wsg_ctx* c, const uint8_t* d_payload, const wsg_send_desc* 
         WSG_HIP(hipMemsetAsync(d_wire_off, 0, sizeof(uint64_t), s));
         return WSG_OK;
     }
-    if (int rc = ensure_enc(c->enc, n, wire_cap))
+    if (int rc = ensure_enc(c, c->enc, n, wire_cap))
         return rc;
     return encode_launch(c, s, d_payload, d_desc, n, d_wire, wire_cap, d_wire_off, c->enc);
 }
@@ -738,7 +750,7 @@ int slot_reserve_enc(wsg_ctx::Slot& sl, uint64_t payload_bytes, uint64_t wire_by
         return rc;
     if (int rc = ensure_array(sl.d_woff, sl.woff_cap, uint64_t(frames) + 1))
         return rc;
-    if (int rc = ensure_enc(sl.enc, frames, wire_bytes))
+    if (int rc = ensure_enc(nullptr, sl.enc, frames, wire_bytes))   // both paths: segments differ
         return rc;
     if (frames > sl.h_desc_cap) {
         if (sl.h_desc)

@@ -1117,16 +1117,20 @@ __device__ __forceinline__ v4u small_bytes(v4u head, const SmallFrame& f, uint64
     return out;
 }
 
+// Also finalizes the frame offsets (k_encode_finalize's job for the piece
+// path): wire_off holds block-local offsets from k_encode_scan_local, plus
+// block_prefix[i / SCAN_ITEMS] from k_encode_scan_blocks.
 __global__ __launch_bounds__(BLOCK) void k_encode_small(const uint8_t* __restrict__ payload,
                                                         const wsg_send_desc* __restrict__ desc, uint32_t n,
-                                                        uint32_t fpb, const uint64_t* __restrict__ wire_off,
-                                                        uint8_t* __restrict__ wire, uint64_t wire_cap)
+                                                        uint32_t fpb, uint64_t* __restrict__ wire_off,
+                                                        const uint64_t* __restrict__ block_prefix,
+                                                        uint8_t* __restrict__ wire, uint64_t wire_cap,
+                                                        unsigned long long* err)
 {
     __shared__ uint64_t s_off[SMALL_F + 1];
     __shared__ v4u s_head[SMALL_F];
     __shared__ SmallFrame s_fr[SMALL_F];
-    if (wire_off[n] > wire_cap)
-        return;   // capacity error latched by k_encode_finalize
+    const bool over = wire_off[n] > wire_cap;   // total, from k_encode_scan_blocks
     const uint32_t f_lo = blockIdx.x * fpb;   // fpb <= SMALL_F (host)
     if (f_lo >= n)
         return;
@@ -1146,11 +1150,19 @@ __global__ __launch_bounds__(BLOCK) void k_encode_small(const uint8_t* __restric
         s_head[t] = h;
         s_fr[t] = SmallFrame{reinterpret_cast<uintptr_t>(payload + d.src_off), d.key,
                              (g.hdr + g.prefix) | (g.hdr << 8)};
-        s_off[t] = wire_off[i];
+        const uint64_t off = wire_off[i] + block_prefix[i / SCAN_ITEMS];
+        const uint64_t end = off + g.hdr + g.body;
+        wire_off[i] = off;
+        s_off[t] = off;
+        if (t + 1 == cnt)
+            s_off[cnt] = end;   // not from wire_off[i + 1]: the next block may have finalized it already
+        if (end > wire_cap)
+            atomicMin(err, (static_cast<unsigned long long>(i) << 8) |
+                               static_cast<unsigned long long>(-WSG_ENOMEM));
     }
-    if (threadIdx.x == 0)
-        s_off[cnt] = wire_off[f_lo + cnt];
     __syncthreads();
+    if (over)
+        return;   // offsets are final and the error latched; no frame bytes
     const uint64_t r_lo = s_off[0], r_hi = s_off[cnt];
     for (uint64_t p = (r_lo & ~uint64_t(CHUNK - 1)) + uint64_t(threadIdx.x) * CHUNK; p < r_hi;
          p += uint64_t(BLOCK) * CHUNK) {
@@ -1383,8 +1395,19 @@ hipError_t launch_encode_mask(hipStream_t s, int grid, const uint8_t* payload, c
     return hipGetLastError();
 }
 
+hipError_t launch_encode_scan_small(hipStream_t s, const wsg_send_desc* desc, uint32_t n, uint64_t* wire_off,
+                                    uint32_t* piece_start, uint64_t* scan)
+{
+    const uint32_t nb = uint32_t((n + SCAN_ITEMS - 1) / SCAN_ITEMS);
+    k_encode_scan_local<<<nb, BLOCK, 0, s>>>(desc, n, wire_off, piece_start, scan, scan + nb);
+    k_encode_scan_blocks<<<1, BLOCK, 0, s>>>(scan, scan + nb, nb, scan + 2 * uint64_t(nb), scan + 3 * uint64_t(nb),
+                                             wire_off, piece_start, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_encode_small(hipStream_t s, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
-                               const uint64_t* wire_off, uint8_t* wire, uint64_t wire_cap)
+                               uint64_t* wire_off, const uint64_t* scan, uint8_t* wire, uint64_t wire_cap,
+                               unsigned long long* err)
 {
     // frames per block: as many as fit SMALL_RANGE wire bytes at the average
     // frame size (wire_cap / n), so that larger frames still fill the grid
@@ -1392,7 +1415,9 @@ hipError_t launch_encode_small(hipStream_t s, const uint8_t* payload, const wsg_
     uint32_t fpb = SMALL_F;
     while (fpb > 1 && uint64_t(fpb) * avg > SMALL_RANGE)
         fpb >>= 1;
-    k_encode_small<<<(n + fpb - 1) / fpb, BLOCK, 0, s>>>(payload, desc, n, fpb, wire_off, wire, wire_cap);
+    const uint32_t nb = uint32_t((n + SCAN_ITEMS - 1) / SCAN_ITEMS);
+    k_encode_small<<<(n + fpb - 1) / fpb, BLOCK, 0, s>>>(payload, desc, n, fpb, wire_off, scan + 2 * uint64_t(nb),
+                                                         wire, wire_cap, err);
     return hipGetLastError();
 }
 

@@ -199,6 +199,10 @@ def test_encode_small_and_piece_kernels(codec, case):
         desc["len"][rng.choice(3000, 6, replace=False)] = [65535, 65536, 65537, 65535, 65536, 70000]
         desc["src_off"] = rng.integers(0, 16, 3000).astype(np.uint64)
         payload = wl.random_bytes(rng, 70016)
+    _both_encode_kernels(codec, payload, desc)
+
+
+def _both_encode_kernels(codec, payload, desc):
     n = len(desc)
     wire_o, off_o = oracle.encode_batch(payload, desc)
     exact = int(off_o[n])
@@ -208,6 +212,20 @@ def test_encode_small_and_piece_kernels(codec, case):
         assert rc == 0
         assert np.array_equal(off_g, off_o), cap
         assert np.array_equal(wire_g, wire_o), cap
+
+
+def test_encode_small_lookback_many_blocks(codec):
+    """k_encode_small computes frame offsets in the same launch (block scan +
+    decoupled look-back): batches of thousands of blocks, back to back with
+    different block counts (the look-back state alternates between launches)."""
+    rng = np.random.default_rng(77)
+    for n, lo, hi in [(300000, 0, 40), (1000, 0, 10), (100000, 0, 2000), (300000, 30, 34), (7, 0, 3)]:
+        payload, desc = _mixed_desc(rng, n, lo, hi)
+        wire_o, off_o = oracle.encode_batch(payload, desc)
+        rc, wire_g, off_g = gpu_encode(codec, payload, desc)
+        assert rc == 0
+        assert np.array_equal(off_g, off_o), n
+        assert np.array_equal(wire_g, wire_o), n
 
 
 # ------------------------------------------- k_decode tile paths (one launch)

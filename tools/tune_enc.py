@@ -6,6 +6,7 @@ usage: CFG=c5|c3|c4 python tools/tune_enc.py [NAME=VALUE@]path/to/libwsg.so ...
 import os
 import statistics
 import sys
+import time
 
 import numpy as np
 import torch
@@ -41,7 +42,7 @@ def main():
     woff = torch.empty(n + 1, dtype=torch.int64, device="cuda")
     codecs = [make_codec(l) for l in libs]
     kern = [[] for _ in libs]
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    step = [[] for _ in libs]   # whole wsg_encode_batch (scan included), 32 calls back to back, wall clock
     for rep in range(int(os.environ.get("REPS", 5))):
         for ci, c in enumerate(codecs):
             for it in range(3):
@@ -53,11 +54,17 @@ def main():
             ms, k = c.timing_read()
             c.timing(False)
             kern[ci].append(ms / k)
+            c.sync()
+            t0 = time.perf_counter()
+            for it in range(32):
+                c.encode_batch(p[it & 1], d, wire=wires[it & 1], wire_cap=cap, wire_off=woff)
+            c.sync()
+            step[ci].append((time.perf_counter() - t0) / 32 * 1e3)
     alg = len(payload) + cap
-    for l, k in zip(libs, kern):
+    for l, k, st in zip(libs, kern, step):
         m = statistics.median(k)
-        print("%-50s encode kernel %.4f ms  %.0f GB/s  spread %.1f%%" % (l, m, alg / m / 1e6,
-                                                                       100 * (max(k) - min(k)) / m))
+        print("%-50s encode kernel %.4f ms  %.0f GB/s  spread %.1f%%  | whole call %.4f ms" % (
+            l, m, alg / m / 1e6, 100 * (max(k) - min(k)) / m, statistics.median(st)))
 
 
 def fanout(libs):
