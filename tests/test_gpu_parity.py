@@ -214,10 +214,10 @@ def _both_encode_kernels(codec, payload, desc):
         assert np.array_equal(wire_g, wire_o), cap
 
 
-def test_encode_small_lookback_many_blocks(codec):
-    """k_encode_small computes frame offsets in the same launch (block scan +
-    decoupled look-back): batches of thousands of blocks, back to back with
-    different block counts (the look-back state alternates between launches)."""
+def test_encode_small_many_blocks(codec):
+    """k_encode_small finalizes the scan's block-local frame offsets itself:
+    batches of thousands of blocks and scan blocks, back to back with
+    different sizes on one context."""
     rng = np.random.default_rng(77)
     for n, lo, hi in [(300000, 0, 40), (1000, 0, 10), (100000, 0, 2000), (300000, 30, 34), (7, 0, 3)]:
         payload, desc = _mixed_desc(rng, n, lo, hi)
