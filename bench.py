@@ -328,6 +328,51 @@ def session_batch_leg(timeout=240):
     return out
 
 
+def echo_size_leg(w, n=1 << 20, size=32, reps=20):
+    """Echo-sized frames on the device batch paths (SURVEY C1's 32 B messages,
+    38 B masked client frames): one batch of 1 Mi frames encoded
+    (wsg_encode_batch: sizes scan + k_encode_small) and the resulting wire
+    decoded (wsg_decode_batch: k_decode, staged tiles), each call timed back to
+    back, inputs in HBM.  A context, not the headline."""
+    import time
+
+    import cppserver_amd as ca
+    from cppserver_amd import workloads as wl
+
+    t = w.torch
+    c = w.codec
+    payload, desc = wl.c3_batch(n, size, size, seed=77)
+    dev = w.wire.device
+    p = t.from_numpy(payload).to(dev)
+    d = ca.desc_to_tensor(desc, dev)
+    cap = n * ca.frame_size(0x82, True, size)
+    wire = t.empty(cap, dtype=t.uint8, device=dev)
+    woff = t.empty(n + 1, dtype=t.int64, device=dev)
+    out = t.empty_like(wire)
+    info = t.empty(n * ca.RECV_INFO.itemsize, dtype=t.uint8, device=dev)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        c.sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        c.sync()
+        return (time.perf_counter() - t0) / reps
+
+    te = timed(lambda: c.encode_batch(p, d, wire=wire, wire_cap=cap, wire_off=woff))
+    ok = int(woff[-1].item()) == cap
+    td = timed(lambda: c.decode_batch(wire, woff[:-1], out=out, info=info))
+    i = n // 2
+    s0 = int(woff[i].item())
+    ok = ok and t.equal(out[s0 + 6: s0 + 38].cpu(), p[i * size: (i + 1) * size].cpu())
+    return {"workload": "%d frames x %d B payload, masked (echo size), device-resident" % (n, size),
+            "encode_us": round(te * 1e6, 1), "decode_us": round(td * 1e6, 1),
+            "encode_Gframes_per_s": round(n / te / 1e9, 2), "decode_Gframes_per_s": round(n / td / 1e9, 2),
+            "roundtrip_ok": bool(ok)}
+
+
 def gather_leg(w, world, device):
     """C5's exchange step: every rank's framed output to rank 0 over RCCL
     (variable-size grouped send/recv, cppserver_amd.shard.gather_frames),
@@ -413,6 +458,7 @@ def main():
         if pc is not None:
             extras["pcie_inclusive_GiBps"] = pc
         if w.cfg == "c2":
+            extras["echo_size_device"] = echo_size_leg(w)
             sb = session_batch_leg()
             if sb is not None:
                 extras["session_batch"] = sb
