@@ -373,6 +373,34 @@ def echo_size_leg(w, n=1 << 20, size=32, reps=20):
             "roundtrip_ok": bool(ok)}
 
 
+def fanout_graph_leg(w, per_graph=20, replays=10):
+    """C4 is launch-latency sensitive: the same fan-out captured
+    `per_graph` times in one HIP graph (torch.cuda.CUDAGraph over the
+    library's launches on the capturing stream) and replayed; reports the
+    fan-out time per call inside the graph next to the eager step."""
+    t = w.torch
+    c = w.codec
+    wires = [w.wire, t.empty_like(w.wire)]
+    for i in range(3):   # nothing is allocated inside a fan-out call; warm anyway
+        c.fanout(w.payload, w.keys, 0x82, True, wire=wires[i & 1])
+    t.cuda.synchronize()
+    g = t.cuda.CUDAGraph()
+    with t.cuda.graph(g):
+        for i in range(per_graph):
+            c.fanout(w.payload, w.keys, 0x82, True, wire=wires[i & 1])
+    g.replay()
+    t.cuda.synchronize()
+    e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(replays):
+        g.replay()
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / (replays * per_graph)
+    return {"fanouts_per_graph": per_graph, "us_per_fanout": round(us, 2),
+            "GiBps": round(w.payload_bytes / (us * 1e-6) / GIB, 1)}
+
+
 def gather_leg(w, world, device):
     """C5's exchange step: every rank's framed output to rank 0 over RCCL
     (variable-size grouped send/recv, cppserver_amd.shard.gather_frames),
@@ -457,6 +485,8 @@ def main():
         pc = pcie_inclusive(w)
         if pc is not None:
             extras["pcie_inclusive_GiBps"] = pc
+        if w.cfg == "c4":
+            extras["hip_graph"] = fanout_graph_leg(w)
         if w.cfg == "c2":
             extras["echo_size_device"] = echo_size_leg(w)
             sb = session_batch_leg()
