@@ -406,7 +406,7 @@ int encode_launch(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, const wsg
                   uint8_t* d_wire, uint64_t wire_cap, uint64_t* d_wire_off, wsg_enc_scratch& e)
 {
     if (small_path(c, n, wire_cap)) {   // sizes scan, then one block per group of frames
-        WSG_HIP(wsg::launch_encode_scan_small(s, d_desc, n, d_wire_off, e.d_piece_start, e.d_scan));
+        WSG_HIP(wsg::launch_encode_scan_small(s, d_desc, n, d_wire_off, e.d_scan));
         const int t = timing_begin(c, s);
         WSG_HIP(wsg::launch_encode_small(s, d_payload, d_desc, n, d_wire_off, e.d_scan, d_wire, wire_cap, c->d_err));
         timing_end(c, s, t);

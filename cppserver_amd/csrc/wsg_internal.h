@@ -61,10 +61,11 @@ hipError_t launch_encode_scan(hipStream_t s, const wsg_send_desc* desc, uint32_t
 hipError_t launch_encode_mask(hipStream_t s, int grid, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
                               const uint64_t* wire_off, const uint32_t* piece_start, const uint32_t* piece_frame,
                               uint8_t* wire, uint64_t wire_cap);
-// Small-frame batch encode: sizes scan without the piece map (scan: as for
-// launch_encode_scan), then k_encode_small, which also finalizes wire_off.
+// Small-frame batch encode: block-local sizes scan (scan: ceil(n /
+// SCAN_ITEMS) block totals), then k_encode_small, which adds the block
+// prefixes, writes the final wire_off[0..n] and latches capacity errors.
 hipError_t launch_encode_scan_small(hipStream_t s, const wsg_send_desc* desc, uint32_t n, uint64_t* wire_off,
-                                    uint32_t* piece_start, uint64_t* scan);
+                                    uint64_t* scan);
 hipError_t launch_encode_small(hipStream_t s, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
                                uint64_t* wire_off, const uint64_t* scan, uint8_t* wire, uint64_t wire_cap,
                                unsigned long long* err);

@@ -820,45 +820,51 @@ __device__ __forceinline__ uint64_t pieces_of(uint64_t frame_bytes)
 } // namespace
 
 // Per-block local exclusive scans of frame sizes and piece counts
-// (SCAN_ITEMS frames per block).
+// (SCAN_ITEMS frames per block).  Round k of a block reads frames
+// k * BLOCK + t, so consecutive lanes read consecutive descriptors (a lane
+// reading SCAN_PER_LANE adjacent descriptors touched 64 lines per load
+// instruction); the rounds scan in frame order, carrying the running sums.
+// PIECES = false (small-frame path): no piece counts.
+template <bool PIECES>
 __global__ __launch_bounds__(BLOCK) void k_encode_scan_local(const wsg_send_desc* __restrict__ desc, uint32_t n,
                                                              uint64_t* __restrict__ wire_off,
                                                              uint32_t* __restrict__ piece_start,
                                                              uint64_t* __restrict__ block_sums,
                                                              uint64_t* __restrict__ block_psums)
 {
-    const uint64_t first = uint64_t(blockIdx.x) * SCAN_ITEMS + uint64_t(threadIdx.x) * SCAN_PER_LANE;
-    uint64_t sz[SCAN_PER_LANE], pc[SCAN_PER_LANE];
-    uint64_t mine = 0, mine_p = 0;
+    const uint64_t first = uint64_t(blockIdx.x) * SCAN_ITEMS;
+    uint64_t sz[SCAN_PER_LANE];
 #pragma unroll
-    for (int k = 0; k < SCAN_PER_LANE; ++k) {
-        const uint64_t i = first + k;
-        sz[k] = pc[k] = 0;
+    for (int k = 0; k < SCAN_PER_LANE; ++k) {   // all descriptor loads first
+        const uint64_t i = first + uint64_t(k) * BLOCK + threadIdx.x;
+        sz[k] = 0;
         if (i < n) {
-            const wsg_send_desc d = desc[i];
-            const SendGeom g = send_geom(d.opcode, d.mask != 0, d.len, d.status);
+            const Desc d = load_desc(desc + i);
+            const SendGeom g = send_geom(d.opcode, d.mask, d.len, d.status);
             sz[k] = g.hdr + g.body;
-            pc[k] = pieces_of(sz[k]);
         }
-        mine += sz[k];
-        mine_p += pc[k];
     }
-    uint64_t total, total_p;
-    uint64_t run = block_exclusive_scan(mine, &total);
-    uint64_t run_p = block_exclusive_scan(mine_p, &total_p);
+    uint64_t run = 0, run_p = 0;
 #pragma unroll
     for (int k = 0; k < SCAN_PER_LANE; ++k) {
-        const uint64_t i = first + k;
+        const uint64_t i = first + uint64_t(k) * BLOCK + threadIdx.x;
+        uint64_t tot, tot_p = 0;
+        const uint64_t ex = block_exclusive_scan(sz[k], &tot);
+        uint64_t ex_p = 0;
+        if (PIECES)
+            ex_p = block_exclusive_scan(sz[k] ? pieces_of(sz[k]) : 0, &tot_p);
         if (i < n) {
-            wire_off[i] = run;
-            piece_start[i] = uint32_t(run_p);
+            wire_off[i] = run + ex;
+            if (PIECES)
+                piece_start[i] = uint32_t(run_p + ex_p);
         }
-        run += sz[k];
-        run_p += pc[k];
+        run += tot;
+        run_p += tot_p;
     }
     if (threadIdx.x == 0) {
-        block_sums[blockIdx.x] = total;
-        block_psums[blockIdx.x] = total_p;
+        block_sums[blockIdx.x] = run;
+        if (PIECES)
+            block_psums[blockIdx.x] = run_p;
     }
 }
 
@@ -1097,6 +1103,8 @@ __device__ __forceinline__ v4u fan_frame_bytes(const uint8_t* __restrict__ paylo
 // two ends of the range, shared with the neighbouring blocks, get byte stores
 // of this block's bytes only.  Correct for any sizes; the host picks it when
 // the average frame is small (SMALL_AVG).
+static_assert(SMALL_F <= BLOCK && SCAN_ITEMS % SMALL_F == 0, "k_encode_small: one frame per lane, one scan block");
+
 struct SmallFrame {
     uint64_t src;   // address of the first data byte
     uint32_t key;
@@ -1117,28 +1125,46 @@ __device__ __forceinline__ v4u small_bytes(v4u head, const SmallFrame& f, uint64
     return out;
 }
 
-// Also finalizes the frame offsets (k_encode_finalize's job for the piece
-// path): wire_off holds block-local offsets from k_encode_scan_local, plus
-// block_prefix[i / SCAN_ITEMS] from k_encode_scan_blocks.
+// Also finishes the offsets scan (k_encode_scan_blocks and
+// k_encode_finalize for the piece path): wire_off holds the block-local
+// offsets of k_encode_scan_local<false>, block_sums its nb block totals; a
+// block's frames share one scan block (fpb divides SCAN_ITEMS), whose prefix
+// the block sums from the L2-resident totals itself.
 __global__ __launch_bounds__(BLOCK) void k_encode_small(const uint8_t* __restrict__ payload,
                                                         const wsg_send_desc* __restrict__ desc, uint32_t n,
                                                         uint32_t fpb, uint64_t* __restrict__ wire_off,
-                                                        const uint64_t* __restrict__ block_prefix,
+                                                        const uint64_t* __restrict__ block_sums, uint32_t nb,
                                                         uint8_t* __restrict__ wire, uint64_t wire_cap,
                                                         unsigned long long* err)
 {
     __shared__ uint64_t s_off[SMALL_F + 1];
     __shared__ v4u s_head[SMALL_F];
     __shared__ SmallFrame s_fr[SMALL_F];
-    const bool over = wire_off[n] > wire_cap;   // total, from k_encode_scan_blocks
     const uint32_t f_lo = blockIdx.x * fpb;   // fpb <= SMALL_F (host)
     if (f_lo >= n)
         return;
+    const uint32_t sb = f_lo / uint32_t(SCAN_ITEMS);
     const uint32_t cnt = min(n - f_lo, fpb);
-    for (uint32_t t = threadIdx.x; t < cnt; t += BLOCK) {
-        const uint32_t i = f_lo + t;
-        const Desc d = load_desc(desc + i);
+    const uint32_t t = threadIdx.x;   // frame f_lo + t (cnt <= BLOCK)
+    // every load first (scan-block totals, descriptor, local offset), so that
+    // their round trips overlap
+    constexpr int PB = 4;   // totals per lane in one go (1 Mi frames); more in the loop below
+    uint64_t bs[PB];
+#pragma unroll
+    for (int u = 0; u < PB; ++u) {
+        const uint32_t k = t + uint32_t(u) * BLOCK;
+        bs[u] = k < nb ? block_sums[k] : 0;
+    }
+    Desc d{};
+    uint64_t off_local = 0;
+    if (t < cnt) {
+        d = load_desc(desc + f_lo + t);
+        off_local = wire_off[f_lo + t];
+    }
+    uint64_t sz = 0;
+    if (t < cnt) {
         const SendGeom g = send_geom(d.opcode, d.mask, d.len, d.status);
+        sz = g.hdr + g.body;
         v4u h = {0, 0, 0, 0};
 #pragma unroll 1
         for (uint32_t r = 0; r < g.hdr; ++r)
@@ -1150,8 +1176,28 @@ __global__ __launch_bounds__(BLOCK) void k_encode_small(const uint8_t* __restric
         s_head[t] = h;
         s_fr[t] = SmallFrame{reinterpret_cast<uintptr_t>(payload + d.src_off), d.key,
                              (g.hdr + g.prefix) | (g.hdr << 8)};
-        const uint64_t off = wire_off[i] + block_prefix[i / SCAN_ITEMS];
-        const uint64_t end = off + g.hdr + g.body;
+    }
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int u = 0; u < PB; ++u) {
+        all += bs[u];
+        before += t + uint32_t(u) * BLOCK < sb ? bs[u] : 0;
+    }
+    for (uint32_t k = t + PB * BLOCK; k < nb; k += BLOCK) {
+        const uint64_t v = block_sums[k];
+        all += v;
+        before += k < sb ? v : 0;
+    }
+    uint64_t prefix, total;
+    (void)block_exclusive_scan(before, &prefix);
+    (void)block_exclusive_scan(all, &total);
+    if (blockIdx.x == 0 && t == 0)
+        wire_off[n] = total;
+    const bool over = total > wire_cap;
+    if (t < cnt) {
+        const uint32_t i = f_lo + t;
+        const uint64_t off = off_local + prefix;
+        const uint64_t end = off + sz;
         wire_off[i] = off;
         s_off[t] = off;
         if (t + 1 == cnt)
@@ -1380,7 +1426,7 @@ hipError_t launch_encode_scan(hipStream_t s, const wsg_send_desc* desc, uint32_t
     uint64_t* psums = scan + nb;
     uint64_t* prefix = scan + 2 * uint64_t(nb);
     uint64_t* pprefix = scan + 3 * uint64_t(nb);
-    k_encode_scan_local<<<nb, BLOCK, 0, s>>>(desc, n, wire_off, piece_start, sums, psums);
+    k_encode_scan_local<true><<<nb, BLOCK, 0, s>>>(desc, n, wire_off, piece_start, sums, psums);
     k_encode_scan_blocks<<<1, BLOCK, 0, s>>>(sums, psums, nb, prefix, pprefix, wire_off, piece_start, n);
     k_encode_finalize<<<(n + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(desc, n, wire_off, piece_start, prefix, pprefix,
                                                                 piece_frame, pieces_cap, wire_cap, err);
@@ -1396,12 +1442,10 @@ hipError_t launch_encode_mask(hipStream_t s, int grid, const uint8_t* payload, c
 }
 
 hipError_t launch_encode_scan_small(hipStream_t s, const wsg_send_desc* desc, uint32_t n, uint64_t* wire_off,
-                                    uint32_t* piece_start, uint64_t* scan)
+                                    uint64_t* scan)
 {
     const uint32_t nb = uint32_t((n + SCAN_ITEMS - 1) / SCAN_ITEMS);
-    k_encode_scan_local<<<nb, BLOCK, 0, s>>>(desc, n, wire_off, piece_start, scan, scan + nb);
-    k_encode_scan_blocks<<<1, BLOCK, 0, s>>>(scan, scan + nb, nb, scan + 2 * uint64_t(nb), scan + 3 * uint64_t(nb),
-                                             wire_off, piece_start, n);
+    k_encode_scan_local<false><<<nb, BLOCK, 0, s>>>(desc, n, wire_off, nullptr, scan, nullptr);
     return hipGetLastError();
 }
 
@@ -1416,8 +1460,8 @@ hipError_t launch_encode_small(hipStream_t s, const uint8_t* payload, const wsg_
     while (fpb > 1 && uint64_t(fpb) * avg > SMALL_RANGE)
         fpb >>= 1;
     const uint32_t nb = uint32_t((n + SCAN_ITEMS - 1) / SCAN_ITEMS);
-    k_encode_small<<<(n + fpb - 1) / fpb, BLOCK, 0, s>>>(payload, desc, n, fpb, wire_off, scan + 2 * uint64_t(nb),
-                                                         wire, wire_cap, err);
+    k_encode_small<<<(n + fpb - 1) / fpb, BLOCK, 0, s>>>(payload, desc, n, fpb, wire_off, scan, nb, wire, wire_cap,
+                                                         err);
     return hipGetLastError();
 }
 
