@@ -139,7 +139,11 @@ __device__ __forceinline__ void store_partial(uint8_t* dst, v4u w, uint32_t nbyt
         dst[j] = uint8_t(lane_byte(w, j));
 }
 
-constexpr int LDSF = BLOCK;   // frames a tile may touch and still take the LDS-staged path
+#ifndef WSG_STAGE_FPL
+#define WSG_STAGE_FPL 2
+#endif
+constexpr int SPL = WSG_STAGE_FPL;   // staged frames per lane per round
+constexpr int LDSF = BLOCK * SPL;    // frames per staged round (one round for tiles of 32-byte frames)
 
 __device__ __forceinline__ uint64_t lane_bcast(uint64_t v, int src)
 {
@@ -535,24 +539,39 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
         // stage the segments of frames r0, r0 + 1, ... that touch the tile;
         // more = frames past the stage touch it too (block-uniform)
         auto stage = [&](uint64_t r0, int& cnt, bool& more) {
-            const uint64_t fi = r0 + threadIdx.x;
-            uint64_t sj = ~uint64_t(0), lim = wire_len;
-            if (fi < n) {
-                sj = fs[fi];
-                lim = fi + 1 < n ? fs[fi + 1] : wire_len;
+            // slot q * BLOCK + lane holds frame r0 + q * BLOCK + lane
+            uint64_t sj[SPL], lim[SPL];
+            bool touch[SPL];
+#pragma unroll
+            for (int q = 0; q < SPL; ++q) {
+                const uint64_t fi = r0 + uint64_t(q) * BLOCK + threadIdx.x;
+                sj[q] = ~uint64_t(0);
+                lim[q] = wire_len;
+                if (fi < n) {
+                    sj[q] = fs[fi];
+                    lim[q] = fi + 1 < n ? fs[fi + 1] : wire_len;
+                }
+                // frame `first` touches (c > MAXF); the others when they start in the tile
+                touch[q] = fi < n && (fi == L.first || sj[q] < tend);
             }
-            // frame `first` touches (c > MAXF); the others when they start in the tile
-            const bool touch = fi < n && (fi == L.first || sj < tend);
             __syncthreads();   // the previous readers are done with the stage
-            cnt = __syncthreads_count(touch);
-            more = __syncthreads_or(threadIdx.x == LDSF - 1 && touch && fi + 1 < n && lim < tend);
-            if (int(threadIdx.x) < cnt) {
-                wsg_recv_info r;
-                frame_parse(wire, wire_len, sj, lim, r);
-                const Seg g = tile_seg(r.payload_off, r.payload_off + r.len, r.key, base, span);
-                s_lo[threadIdx.x] = g.lo;
-                s_hi[threadIdx.x] = g.hi;
-                s_kr[threadIdx.x] = g.kr;
+            cnt = 0;
+#pragma unroll
+            for (int q = 0; q < SPL; ++q)
+                cnt += __syncthreads_count(touch[q]);
+            more = __syncthreads_or(threadIdx.x == BLOCK - 1 && touch[SPL - 1] &&
+                                    r0 + uint64_t(LDSF) < n && lim[SPL - 1] < tend);
+#pragma unroll 1
+            for (int q = 0; q < SPL; ++q) {
+                const int slot = q * BLOCK + int(threadIdx.x);
+                if (slot < cnt) {
+                    wsg_recv_info r;
+                    frame_parse(wire, wire_len, sj[q], lim[q], r);
+                    const Seg g = tile_seg(r.payload_off, r.payload_off + r.len, r.key, base, span);
+                    s_lo[slot] = g.lo;
+                    s_hi[slot] = g.hi;
+                    s_kr[slot] = g.kr;
+                }
             }
             __syncthreads();
         };
