@@ -140,6 +140,16 @@ def test_uniform_sizes_vs_oracle(codec, size):
     assert_decode_parity(codec, wire, fs)
 
 
+@pytest.mark.parametrize("size", [58, 57, 26, 25, 10, 0])
+def test_decode_staged_round_sizes(codec, size):
+    """Staged tiles hold 512 frames per round (two per lane): masked frames
+    of 64 B (256 per 16 KiB tile), 63 B, 32 B (exactly 512: one round), 31 B
+    (528: a second round), 16 B (1024) and 6 B (2730) per frame."""
+    wire, fs, _ = wl.c2_wire(6000, size, seed=1000 + size)
+    assert_decode_parity(codec, wire, fs)
+    assert_decode_parity(codec, wire, fs, inplace=True)
+
+
 # ---------------------------------------------------------------- ragged / C3
 def _mixed_desc(rng, n, lo, hi):
     lens = rng.integers(lo, hi + 1, n)
