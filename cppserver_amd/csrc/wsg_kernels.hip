@@ -53,6 +53,9 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_DIAG_FAN
 #define WSG_DIAG_FAN 0   // timing-only fan-out diagnostics: 1 no key loads, 2 no payload loads, 4 stores only, 8 no edge blocks
 #endif
+#ifndef WSG_DIAG_NOINFO
+#define WSG_DIAG_NOINFO 0   // timing-only: k_decode without its per-frame info slice (tools/)
+#endif
 #ifndef WSG_DEC_WAVES
 #define WSG_DEC_WAVES 1   // k_decode minimum waves/SIMD (register cap); 6 and 8 spill and run slower
 #endif
@@ -437,7 +440,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
 {
     // per-frame slice: header unpack + checks, one lane per frame
     const uint64_t fstride = uint64_t(gridDim.x) * BLOCK;
-    for (uint64_t i0 = uint64_t(blockIdx.x) * BLOCK + (threadIdx.x & ~63u); i0 < n; i0 += fstride) {
+    for (uint64_t i0 = uint64_t(blockIdx.x) * BLOCK + (threadIdx.x & ~63u); i0 < n && !WSG_DIAG_NOINFO;
+         i0 += fstride) {
         const uint64_t i = i0 + (threadIdx.x & 63u);
         if (i < n) {
             wsg_recv_info r;
