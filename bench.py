@@ -158,7 +158,8 @@ class Workload:
             self.wire = torch.empty(fsz * k, dtype=torch.uint8, device=device)
             self.payload_bytes = length * k
             self.alg_bytes = fsz * k + length + 4 * k
-            self.kernel = "k_fanout_flat"
+            # frame sizes that are a multiple of 4 take the period kernel (wsg_kernels.hip launch_fanout_period)
+            self.kernel = "k_fanout_period" if fsz % 4 == 0 else "k_fanout_flat"
             self.workload = "C4 fan-out: one %d B payload masked with %d client keys" % (length, k)
             self.extra = {"keys": k, "wire_bytes": fsz * k}
         else:  # c5: this rank's round-robin shard of 1 Mi x 16 KiB frames, encode

@@ -26,6 +26,7 @@ struct wsg_ctx {
     hipStream_t stream = nullptr;
     int num_cus = 256;
     int blocks_per_cu = 32;   // measured best for the C2 unmask (tools/tune.py)
+    int fan_waves_per_cu = 8;    // fan-out period path: waves per CU (tools/tune_enc.py CFG=c4: 8 best of 4-32)
     uint64_t small_avg = wsg::SMALL_AVG;   // batch encode: k_encode_small when wire_cap <= n * small_avg
     unsigned long long* d_err = nullptr;
     // scratch
@@ -261,6 +262,11 @@ int wsg_create(int device, wsg_ctx** out)
         if (v > 0 && v <= 256)
             c->blocks_per_cu = v;
     }
+    if (const char* e = std::getenv("WSG_FAN_WAVES_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
+        const int v = std::atoi(e);
+        if (v > 0 && v <= 64)
+            c->fan_waves_per_cu = v;
+    }
     if (const char* e = std::getenv("WSG_SMALL_AVG"))   // A/B measurements (tools/tune_enc.py)
         c->small_avg = std::strtoull(e, nullptr, 10);
     *out = c;
@@ -456,6 +462,13 @@ int wsg_fanout_encode(wsg_ctx* c, const uint8_t* d_payload, uint64_t len, const 
         return WSG_ENOMEM;
     hipStream_t s = pick(c, stream);
     const int t = timing_begin(c, s);
+    hipError_t perr = hipSuccess;
+    if (wsg::launch_fanout_period(s, c->num_cus, c->fan_waves_per_cu, d_payload, len, d_keys, k, opcode, mask ? 1u : 0u,
+                                  fsize, d_wire, &perr)) {
+        WSG_HIP(perr);
+        timing_end(c, s, t);
+        return WSG_OK;
+    }
     const uint64_t pieces = uint64_t(k) * ((fsize + wsg::PIECE_ALIGN - 1 + wsg::PIECE - 1) / wsg::PIECE);
     const uint64_t blocks = wsg::fanout_flat ? ceil_div(ceil_div(total, wsg::CHUNK), wsg::BLOCK * wsg::FAN_UNITS)
                                              : ceil_div(pieces, wsg::BLOCK / 64);

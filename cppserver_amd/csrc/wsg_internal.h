@@ -69,6 +69,9 @@ hipError_t launch_encode_scan_small(hipStream_t s, const wsg_send_desc* desc, ui
 hipError_t launch_encode_small(hipStream_t s, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
                                uint64_t* wire_off, const uint64_t* scan, uint8_t* wire, uint64_t wire_cap,
                                unsigned long long* err);
+bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_t* payload, uint64_t len,
+                          const uint32_t* keys, uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize,
+                          uint8_t* wire, hipError_t* err);
 hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64_t len, const uint32_t* keys,
                          uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire);
 hipError_t launch_xor(hipStream_t s, int grid, const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,

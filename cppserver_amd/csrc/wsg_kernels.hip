@@ -51,13 +51,19 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #define WSG_DIAG 0   // 5: timing-only diagnostic build of k_decode (every tile streams; tools/)
 #endif
 #ifndef WSG_DIAG_FAN
-#define WSG_DIAG_FAN 0   // timing-only fan-out diagnostics: 1 no key loads, 2 no payload loads, 4 stores only, 8 no edge blocks
+#define WSG_DIAG_FAN 0   // timing-only fan-out diagnostics: 1 no key loads, 2 no payload loads, 4 stores only, 8 no edge blocks; period path: 16 no template loads, 32 no key loads
 #endif
 #ifndef WSG_DIAG_NOINFO
 #define WSG_DIAG_NOINFO 0   // timing-only: k_decode without its per-frame info slice (tools/)
 #endif
 #ifndef WSG_DEC_WAVES
 #define WSG_DEC_WAVES 1   // k_decode minimum waves/SIMD (register cap); 6 and 8 spill and run slower
+#endif
+#ifndef WSG_FAN_PERIOD
+#define WSG_FAN_PERIOD 1   // fan-out: period path (k_fanout_period) where the frame size allows; 0 = flat kernel only
+#endif
+#ifndef WSG_FAN_KV
+#define WSG_FAN_KV 2   // fan-out period path: key registers per lane (64 pass-window slots each)
 #endif
 #ifndef WSG_NT_STORE
 #define WSG_NT_STORE 1
@@ -1404,6 +1410,84 @@ __global__ __launch_bounds__(BLOCK) void k_fanout_flat(const uint8_t* __restrict
     }
 }
 
+// ---- fan-out, period path ---------------------------------------------------
+// The k frames of a fan-out are one template (header + status + payload) and
+// differ only in the key XORed over fixed byte positions.  With the frame size
+// F a multiple of 4, every P = 16 / gcd(F, 16) (<= 4) consecutive frames form a
+// group of G = P * F / 16 whole chunks, so a chunk's bytes depend only on its
+// position j within its group and on the keys of the (<= 2) frames it touches:
+//     chunk = T[j] ^ (MA[j] & rot(key_a)) ^ (MB[j] & rot(key_b)).
+// With W waves (one per 64-thread block: 4-wave blocks measured slower) and W * 64 a multiple of G, a lane's j
+// is the same in every pass, so it builds T / MA / MB once (the only payload
+// loads) and then only stores, pass after pass, its chunk of successive groups.
+// The wave's keys for all its passes come in one vector load up front (lane
+// q holds key P * (first group of pass q / 2P) + q % 2P) and are picked per
+// pass with a lane shuffle.  Rows are 1 KiB-aligned, whole lines per wave.
+template <int P>
+__global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict__ payload, uint64_t len,
+                                                      const uint32_t* __restrict__ keys, uint32_t k, uint8_t opcode,
+                                                      uint32_t mask, uint64_t fsize, uint32_t G, uint32_t dm,
+                                                      uint8_t* __restrict__ wire)
+{
+    constexpr int KW = 2 * P;   // keys per pass: the row spans <= 2 groups (G >= 64)
+    const FanGeom f = fan_geom(opcode, mask != 0, len);
+    const uint64_t total = fsize * k;
+    const uint64_t chunks = (total + CHUNK - 1) / CHUNK;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wpb = blockDim.x / 64;              // 1, 2 or 4 waves per block (host: W % wpb == 0)
+    const uint64_t row0 = (uint64_t(blockIdx.x) * wpb + threadIdx.x / 64) * 64;
+    const uint64_t rstep = uint64_t(gridDim.x) * wpb * 64;   // W rows: a multiple of G (dm groups)
+    if (row0 >= chunks)
+        return;
+    const uint64_t m0 = row0 / G;                        // first group of pass 0
+    const uint32_t jw = uint32_t(row0 - m0 * G);         // group position of lane 0
+    const uint32_t dl = (jw + lane) >= G ? 1u : 0u;      // lane's group: m0 + dl (+ it * dm)
+    const uint32_t j = jw + lane - dl * G;
+
+    // template of chunk j
+    const uint64_t o = uint64_t(j) * CHUNK;
+    const uint32_t qa = uint32_t(o / fsize);             // frame of the group holding byte o
+    const uint64_t r = o - uint64_t(qa) * fsize;
+    const v4u ta = (WSG_DIAG_FAN & 16) ? v4u{j, 1, 2, 3} : fan_frame_bytes(payload, len, f, fsize, 0u, r);
+    const v4u ma = (WSG_DIAG_FAN & 16) ? v4u{~0u, ~0u, ~0u, ~0u} : ta ^ fan_frame_bytes(payload, len, f, fsize, ~0u, r);
+    const uint64_t split = fsize - r;                    // the next frame starts at chunk byte `split`
+    v4u t = ta, mb = {0, 0, 0, 0};
+    if (split < CHUNK) {
+        const v4u tb = fan_frame_bytes(payload, len, f, fsize, 0u, 0);
+        t ^= shl_bytes(tb, split);
+        mb = shl_bytes(tb ^ fan_frame_bytes(payload, len, f, fsize, ~0u, 0), split);
+    }
+    const uint32_t pa = uint32_t(r - f.g.hdr), pb = uint32_t(0u - uint32_t(split) - f.g.hdr);
+    const uint32_t ia = P * dl + qa;                     // key slots of this pass's window
+
+    // keys of every pass: slot it * KW + q -> key P * (m0 + it * dm) + q
+    const uint64_t passes = (chunks - row0 + rstep - 1) / rstep;   // host: passes * KW <= 64 * WSG_FAN_KV
+    uint32_t kv[WSG_FAN_KV];
+#pragma unroll
+    for (int h = 0; h < WSG_FAN_KV; ++h) {
+        const uint32_t s = uint32_t(h) * 64 + lane;
+        const uint64_t it = s / KW;
+        const uint64_t idx = uint64_t(P) * (m0 + it * dm) + (s % KW);
+        kv[h] = (WSG_DIAG_FAN & 32) ? uint32_t(idx) : (it < passes && idx < k) ? keys[idx] : 0u;
+    }
+
+    for (uint32_t it = 0; it < passes; ++it) {
+        const uint64_t c = row0 + uint64_t(it) * rstep + lane;
+        const uint32_t slot = it * KW;                           // wave-uniform; KW divides 64
+        uint32_t kreg = kv[0];
+#pragma unroll
+        for (int h = 1; h < WSG_FAN_KV; ++h)
+            kreg = (slot >> 6) == uint32_t(h) ? kv[h] : kreg;
+        const uint32_t sb = (slot & 63) * 4;
+        const uint32_t ka = __builtin_amdgcn_ds_bpermute(int(sb + ia * 4), int(kreg));
+        const uint32_t kb = __builtin_amdgcn_ds_bpermute(int(sb + (ia + 1) * 4), int(kreg));
+        const uint32_t ra = key_rot(ka, pa), rb = key_rot(kb, pb);
+        const v4u w = t ^ (ma & v4u{ra, ra, ra, ra}) ^ (mb & v4u{rb, rb, rb, rb});
+        if (c < chunks)
+            fan_store(wire, c, chunks, total, w);
+    }
+}
+
 // Single-buffer XOR used by the per-frame host path: dst[i] = src[i] ^
 // key[(phase + i) % 4].  src/dst 16-byte aligned device staging buffers.
 __global__ __launch_bounds__(BLOCK) void k_xor(const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,
@@ -1502,6 +1586,55 @@ hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64
     else
         k_fanout<<<grid, BLOCK, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, wire);
     return hipGetLastError();
+}
+
+// Period path (k_fanout_period) when the frame size allows it; returns false
+// to leave the batch to k_fanout_flat.  Wave count W = Q * s with W * 64 a
+// multiple of G (Q = G / gcd(G, 64)), about `waves` of them, and few enough
+// passes per wave that one key load covers them (passes * 2P <= 64 * WSG_FAN_KV).
+bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_t* payload, uint64_t len,
+                          const uint32_t* keys, uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize,
+                          uint8_t* wire, hipError_t* err)
+{
+    if (!WSG_FAN_PERIOD || fsize % 4 != 0)
+        return false;
+    uint64_t g16 = 16;
+    while (fsize % g16)
+        g16 >>= 1;
+    const uint32_t P = uint32_t(16 / g16);               // 1, 2 or 4
+    const uint64_t G = uint64_t(P) * fsize / CHUNK;
+    if (G < 64 || G > (1u << 20))
+        return false;
+    uint64_t g64 = 64;
+    while (G % g64)
+        g64 >>= 1;
+    const uint64_t Q = G / g64;
+    const uint64_t chunks = (fsize * k + CHUNK - 1) / CHUNK;
+    const uint64_t max_passes = 64 * WSG_FAN_KV / (2 * P);
+    if (Q * 64 > chunks * 2)   // even the fewest waves would mostly idle: leave it to the flat kernel
+        return false;
+    const uint64_t rows = (chunks + 63) / 64;
+    uint64_t mult = std::max<uint64_t>(1, (uint64_t(cus) * waves_per_cu + Q / 2) / Q);
+    mult = std::min(mult, (rows + Q - 1) / Q);                                                 // no idle waves
+    mult = std::max(mult, (chunks + Q * 64 * max_passes - 1) / (Q * 64 * max_passes));   // one key load
+    const uint64_t W = Q * mult;
+    if (W > (1u << 22))
+        return false;
+    const uint32_t dm = uint32_t(W * 64 / G);
+    const uint64_t wpb = 1;   // waves per block: one (4-wave blocks measured 8 % slower at C4)
+    switch (P) {
+    case 1:
+        k_fanout_period<1><<<uint32_t(W / wpb), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire);
+        break;
+    case 2:
+        k_fanout_period<2><<<uint32_t(W / wpb), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire);
+        break;
+    default:
+        k_fanout_period<4><<<uint32_t(W / wpb), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire);
+        break;
+    }
+    *err = hipGetLastError();
+    return true;
 }
 
 hipError_t launch_xor(hipStream_t s, int grid, const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,

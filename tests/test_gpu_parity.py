@@ -384,6 +384,35 @@ def test_fanout_mid_sizes(codec, length, k, opcode, mask, src_off):
     assert (got[len(ref):] == 0xA5).all()
 
 
+@pytest.mark.parametrize("length,k,opcode,mask,src_off", [
+    (4096, 10000, 0x82, True, 0),   # C4: F = 4104, groups of 2 frames (513 chunks)
+    (4096, 257, 0x82, True, 5),     # odd k: the last group is half a group
+    (4088, 3000, 0x82, True, 0),    # F = 4096: one frame per group
+    (1016, 5000, 0x81, True, 3),    # F = 1024: G = 64, every row is exactly one group
+    (1006, 777, 0x88, True, 0),     # close with status prefix (Q2): F = 1016, G = 127
+    (2040, 1001, 0x82, False, 1),   # unmasked, still XORed (Q1): F = 2044, groups of 4 frames
+    (4096, 4097, 0x82, False, 0),   # F = 4100: 4-frame groups, wire ends inside a chunk
+    (8190, 130, 0x89, True, 8),     # ping with status prefix: F = 8200
+    (65538, 40, 0x82, True, 0),     # 8-byte length form: F = 65552, 4097-chunk groups
+])
+def test_fanout_period_path(codec, length, k, opcode, mask, src_off):
+    """Fan-outs whose frame size is a multiple of 4 take k_fanout_period (one
+    chunk template per lane, keys picked per pass): parity with the oracle,
+    nothing written past the k frames."""
+    payload, keys = wl.c4_fanout(length, k, seed=11 * length + k)
+    ref = oracle.fanout_encode(payload, keys, opcode, mask)
+    assert len(ref) % (4 * k) == 0
+    buf = np.zeros(length + src_off + 1, np.uint8)
+    buf[src_off: src_off + length] = payload
+    wire = torch.full((len(ref) + 48,), 0xA5, dtype=torch.uint8, device="cuda")
+    codec.fanout(dev(buf)[src_off:], dev(keys.view(np.int32)), opcode, mask, wire=wire, length=length)
+    codec.sync()
+    got = wire.cpu().numpy()
+    bad = np.nonzero(got[: len(ref)] != ref)[0]
+    assert bad.size == 0, "first mismatch at byte %d of %d" % (bad[0], len(ref))
+    assert (got[len(ref):] == 0xA5).all()
+
+
 # ---------------------------------------------------------------- edge cases
 def test_empty_batches(codec):
     rc, out, info = gpu_decode(codec, np.zeros(32, np.uint8), [])
