@@ -25,7 +25,9 @@ struct wsg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     int num_cus = 256;
-    int blocks_per_cu = 32;   // measured best for the C2 unmask (tools/tune.py)
+    int blocks_per_cu = 32;       // encode / fan-out / xor grids
+    int enc_blocks_per_cu = 1024; // k_encode_mask grid, ~1-2 pieces per wave (tools/tune_enc.py: C5 share -15 %, C3-like -6 % vs 32)
+    int dec_blocks_per_cu = 48;   // k_decode grid: 40-56 best, 48 chosen (tools/tune.py: C2 -3.5 %, C3 ragged -2 % vs 32)
     int fan_waves_per_cu = 8;    // fan-out period path: waves per CU (tools/tune_enc.py CFG=c4: 8 best of 4-32)
     uint64_t small_avg = wsg::SMALL_AVG;   // batch encode: k_encode_small when wire_cap <= n * small_avg
     unsigned long long* d_err = nullptr;
@@ -105,9 +107,9 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 inline hipStream_t pick(wsg_ctx*, void* s) { return static_cast<hipStream_t>(s); }
 inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
-int grid_for(const wsg_ctx* c, uint64_t tiles)
+int grid_for(const wsg_ctx* c, uint64_t tiles, int blocks_per_cu = 0)
 {
-    const uint64_t cap = uint64_t(c->num_cus) * uint64_t(c->blocks_per_cu);
+    const uint64_t cap = uint64_t(c->num_cus) * uint64_t(blocks_per_cu ? blocks_per_cu : c->blocks_per_cu);
     return int(std::max<uint64_t>(1, std::min(tiles, cap)));
 }
 
@@ -260,7 +262,12 @@ int wsg_create(int device, wsg_ctx** out)
     if (const char* e = std::getenv("WSG_BLOCKS_PER_CU")) {
         const int v = std::atoi(e);
         if (v > 0 && v <= 256)
-            c->blocks_per_cu = v;
+            c->blocks_per_cu = c->dec_blocks_per_cu = c->enc_blocks_per_cu = v;   // A/B runs: every grid
+    }
+    if (const char* e = std::getenv("WSG_ENC_BLOCKS_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
+        const int v = std::atoi(e);
+        if (v > 0 && v <= 4096)
+            c->enc_blocks_per_cu = v;
     }
     if (const char* e = std::getenv("WSG_FAN_WAVES_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
         const int v = std::atoi(e);
@@ -368,7 +375,7 @@ int decode_launch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const ui
     // a short (or empty) wire are still checked
     const uint64_t tiles = ceil_div(wire_len, wsg::TILE);
     const int t = timing_begin(c, s);
-    WSG_HIP(wsg::launch_decode(s, grid_for(c, std::max(tiles, ceil_div(n, wsg::BLOCK))), d_wire, d_out, wire_len,
+    WSG_HIP(wsg::launch_decode(s, grid_for(c, std::max(tiles, ceil_div(n, wsg::BLOCK)), c->dec_blocks_per_cu), d_wire, d_out, wire_len,
                                d_frame_start, n, d_info, c->d_err));
     timing_end(c, s, t);
     return WSG_OK;
@@ -422,7 +429,7 @@ int encode_launch(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, const wsg
     WSG_HIP(wsg::launch_encode_scan(s, d_desc, n, d_wire_off, e.d_piece_start, e.d_scan, e.d_piece_frame, pieces_cap,
                                     wire_cap, c->d_err));
     const int t = timing_begin(c, s);
-    WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, ceil_div(pieces_cap, wsg::BLOCK / 64)), d_payload, d_desc, n,
+    WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, ceil_div(pieces_cap, wsg::BLOCK / 64), c->enc_blocks_per_cu), d_payload, d_desc, n,
                                     d_wire_off, e.d_piece_start, e.d_piece_frame, d_wire, wire_cap));
     timing_end(c, s, t);
     return WSG_OK;
