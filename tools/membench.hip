@@ -376,6 +376,37 @@ int main(int argc, char** argv)
     printf("device %s CUs=%d bytes=%llu MiB\n", p.gcnArchName, cus, (unsigned long long)mib);
     if (argc > 2 && std::string(argv[2]) == "explore")
         return explore(bytes, cus);
+    if (argc > 2 && std::string(argv[2]) == "grid") {
+        // copy ceiling against the grid: 16 KiB block tiles and 4 KiB wave
+        // pieces, from grid-stride (8 blocks/CU) to one unit per block/wave;
+        // two source/destination pairs used in turn (no warm Infinity Cache)
+        const uint64_t span = 4 * bytes;
+        uint8_t* base;
+        CK(hipMalloc(&base, span));
+        CK(hipMemset(base, 5, span));
+        auto P = [&](uint64_t off) { return (u32x4*)(base + off); };
+        const uint64_t tiles = n16 / (256 * 4), pieces = n16 / (64 * 4);
+        for (int rep = 0; rep < 2; ++rep) {
+            for (uint64_t bpc : {8ull, 32ull, 48ull, 64ull, 128ull, 1024ull}) {
+                const int g1 = int(std::min<uint64_t>(tiles, cus * bpc));
+                double ms = time_kernel([&](int i) {
+                    const uint64_t s = (i & 1) * 2 * bytes;
+                    k_stream<256, 4, 3><<<g1, 256>>>(P(s), P(s + bytes), n16, 9u);
+                });
+                printf("block-tile 16K bpc=%4llu grid=%6d %8.1f us %7.1f GB/s\n", (unsigned long long)bpc, g1, ms * 1e3,
+                       2.0 * bytes / (ms * 1e-3) / 1e9);
+                const int g2 = int(std::min<uint64_t>((pieces + 3) / 4, cus * bpc));
+                ms = time_kernel([&](int i) {
+                    const uint64_t s = (i & 1) * 2 * bytes;
+                    k_wavepiece<256, 4, 3><<<g2, 256>>>(P(s), P(s + bytes), n16, 9u);
+                });
+                printf("wave-piece 4K  bpc=%4llu grid=%6d %8.1f us %7.1f GB/s\n", (unsigned long long)bpc, g2, ms * 1e3,
+                       2.0 * bytes / (ms * 1e-3) / 1e9);
+            }
+        }
+        CK(hipFree(base));
+        return 0;
+    }
     u32x4 *src, *dst;
     CK(hipMalloc(&src, bytes));
     CK(hipMalloc(&dst, bytes));
