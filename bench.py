@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--frames", type=int, default=None)
     ap.add_argument("--size", type=int, default=None)
+    ap.add_argument("--messages", type=int, default=1,
+                    help="c4: messages per fan-out call (wsg_fanout_encode_many; ws_multicast's per-tick batch)")
+    ap.add_argument("--no-c5-job", action="store_true", help="N>1: skip the C5 encode+gather leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip copy-ceiling and PCIe-inclusive legs")
@@ -98,6 +101,36 @@ def pmc_traffic(path, config):
         return None
 
 
+def host_cpu():
+    """The host the CPU baseline runs on: model, CPUs visible, and the
+    threads used (the affinity set, capped by a cgroup CPU quota and by
+    $OMP_NUM_THREADS where the box sets one: a GPU box's CPU share is smaller
+    than the machine nproc reports)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nproc = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    threads = nproc if quota is None else min(nproc, quota)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        threads = min(threads, int(omp))
+    return {"cpu_model": model, "nproc": nproc, "cgroup_cpus": quota, "threads": max(1, threads)}
+
+
 class Workload:
     """Holds device inputs/outputs and runs one step."""
 
@@ -135,6 +168,7 @@ class Workload:
         elif self.cfg == "c3":
             n = args.frames or 65536
             payload, desc = wl.c3_batch(n, 128, args.size or 65536, seed=3000 + rank)
+            self.host = (payload, desc)
             self.payload = torch.from_numpy(payload).to(device)
             self.desc = ca.desc_to_tensor(desc, device)
             cap = int(sum(ca.frame_size(0x82, True, int(x)) for x in desc["len"]))
@@ -151,24 +185,42 @@ class Workload:
         elif self.cfg == "c4":
             k = args.frames or 10000
             length = args.size or 4096
-            payload, keys = wl.c4_fanout(length, k, seed=4000 + rank)
+            m = max(1, args.messages)
+            # m messages of `length` bytes (one random arena) x k client keys
+            rng = np.random.default_rng(4000 + rank)
+            payload = wl.random_bytes(rng, m * length + 16)
+            keys = rng.integers(0, 2**32, k, dtype=np.uint64).astype(np.uint32)
+            self.host = (payload, keys)
+            self.m, self.length = m, length
+            self.src_off = np.arange(m, dtype=np.uint64) * np.uint64(length)
+            self.lens = np.full(m, length, dtype=np.uint64)
+            self.ops = np.full(m, 0x82, dtype=np.uint8)
             self.payload = torch.from_numpy(payload).to(device)
             self.keys = torch.from_numpy(keys.view(np.int32)).to(device)
             fsz = ca.frame_size(0x82, True, length)
-            self.wire = torch.empty(fsz * k, dtype=torch.uint8, device=device)
-            self.payload_bytes = length * k
-            self.alg_bytes = fsz * k + length + 4 * k
+            per_msg = (fsz * k + 127) // 128 * 128
+            self.wire = torch.empty(per_msg * m, dtype=torch.uint8, device=device)
+            self.payload_bytes = m * length * k
+            self.alg_bytes = m * (fsz * k + length + 4 * k)
             # frame sizes that are a multiple of 4 take the period kernel (wsg_kernels.hip launch_fanout_period)
             self.kernel = "k_fanout_period" if fsz % 4 == 0 else "k_fanout_flat"
-            self.workload = "C4 fan-out: one %d B payload masked with %d client keys" % (length, k)
-            self.extra = {"keys": k, "wire_bytes": fsz * k}
+            self.workload = ("C4 fan-out: one %d B payload masked with %d client keys" % (length, k) if m == 1 else
+                             "C4 x %d messages: %d B payloads x %d client keys in one wsg_fanout_encode_many call"
+                             % (m, length, k))
+            self.extra = {"keys": k, "messages": m, "wire_bytes": fsz * k * m}
         else:  # c5: this rank's round-robin shard of 1 Mi x 16 KiB frames, encode
             world = int(os.environ.get("WORLD_SIZE", "1"))
             size = args.size or 16384
-            payload, desc, ids = wl.c5_shard(rank, world, n_total=args.frames or (1 << 20), size=size,
-                                             max_frames=None)
-            self.payload = torch.from_numpy(payload).to(device)
+            n_total = args.frames or (1 << 20)
+            from cppserver_amd import shard
+
+            ids = shard.rank_frames(rank, world, n_total)
+            # payloads are a function of the global frame index, made in HBM
+            # (16 GiB at one GPU); the host regenerates any frame to check it
+            self.payload = wl.c5_payload_torch(ids, size, device=device)
+            desc = wl.c5_desc(ids, size)
             self.desc = ca.desc_to_tensor(desc, device)
+            self.host = (ids, desc, size)
             n = len(desc)
             cap = n * ca.frame_size(0x82, True, size)
             self.wire = torch.empty(cap, dtype=torch.uint8, device=device)
@@ -177,7 +229,7 @@ class Workload:
             self.payload_bytes = n * size
             self.alg_bytes = n * size + cap
             self.kernel = "k_encode_mask"
-            self.workload = "C5 encode shard: %d x %d B frames of a 1 Mi-frame job (round-robin)" % (n, size)
+            self.workload = "C5 encode shard: %d x %d B frames of a %d-frame job (round-robin)" % (n, size, n_total)
             self.extra = {"frames_this_rank": n, "wire_bytes": cap}
 
     def step(self):
@@ -190,56 +242,164 @@ class Workload:
             c.encode_batch(self.payload, self.desc, wire=self.wire, wire_cap=self.cap, wire_off=self.woff)
             c.decode_batch(self.wire, self.woff[:-1], out=self.out, info=self.info)
         elif self.cfg == "c4":
-            c.fanout(self.payload, self.keys, 0x82, True, wire=self.wire)
+            if self.m == 1:
+                c.fanout(self.payload, self.keys, 0x82, True, wire=self.wire, length=self.length)
+            else:
+                c.fanout_many(self.payload, self.src_off, self.lens, self.ops, self.keys, wire=self.wire)
         else:
             c.encode_batch(self.payload, self.desc, wire=self.wire, wire_cap=self.cap, wire_off=self.woff)
 
     def spot_check(self):
-        """Cheap self-check of one step's output (not the oracle)."""
-        if self.cfg != "c2":
-            return True
-        wire, fs, keys = self.host
-        self.codec.decode_batch(self.wire, self.fs, out=self.out, info=self.info)
+        """One step's output at sampled frames against the oracle (the CPU
+        restatement of ws.cpp), after the warm-up: c2 the unmasked payload
+        and header bytes, c3 encode bytes and the decoded payload, c4 sampled
+        fan-out frames, c5 sampled frames of the shard (payload regenerated
+        on the host from the frame index)."""
+        import oracle
+
+        import cppserver_amd as ca
+
+        self.step()
         self.codec.sync()
-        out = self.out.cpu().numpy()
-        n = len(fs)
-        fsz = len(wire) // n
-        ok = True
-        for i in (0, n // 2, n - 1):
-            s = int(fs[i])
-            hdr = fsz - (self.payload_bytes // n)
-            p = wire[s + hdr: s + fsz]
-            kb = np.frombuffer(int(keys[i]).to_bytes(4, "little"), np.uint8)
-            ok &= bool(np.array_equal(out[s + hdr: s + fsz], p ^ np.resize(kb, len(p))))
-            ok &= bool(np.array_equal(out[s: s + hdr], wire[s: s + hdr]))
-        return ok
+        if self.cfg == "c2":
+            _, fs, _ = self.host
+            win, out = self.batches[self.turn ^ 1]   # the batch the step above decoded
+            n = len(fs)
+            fsz = int(win.numel()) // n
+            ok = True
+            for i in (0, n // 2, n - 1):
+                s = int(fs[i])
+                rc, ref, _ = oracle.decode_batch(win[s: s + fsz].cpu().numpy(), np.zeros(1, np.uint64))
+                ok &= rc == 0 and bool(np.array_equal(out[s: s + fsz].cpu().numpy(), ref))
+            return bool(ok)
+        if self.cfg == "c3":
+            payload, desc = self.host
+            n = len(desc)
+            offs = self.woff.cpu().numpy()
+            ok = True
+            for i in (0, 1, n // 2, n - 1):
+                d = desc[i: i + 1].copy()
+                ref, _ = oracle.encode_batch(payload, d)
+                a, b = int(offs[i]), int(offs[i + 1])
+                got = self.wire[a: b].cpu().numpy()
+                dec = self.out[a: b].cpu().numpy()
+                p = payload[int(d["src_off"][0]): int(d["src_off"][0]) + int(d["len"][0])]
+                ok &= bool(np.array_equal(got, ref)) and bool(np.array_equal(dec[len(dec) - len(p):], p))
+            return bool(ok)
+        if self.cfg == "c4":
+            payload, keys = self.host
+            fsz = ca.frame_size(0x82, True, self.length)
+            k = len(keys)
+            per_msg = (fsz * k + 127) // 128 * 128 if self.m > 1 else fsz * k
+            ok = True
+            for mi in sorted({0, self.m - 1}):
+                msg = payload[mi * self.length: (mi + 1) * self.length]
+                for j in (0, 1, k // 2, k - 1):
+                    ref = oracle.fanout_encode(msg, keys[j: j + 1], 0x82, True)
+                    a = mi * per_msg + j * fsz
+                    ok &= bool(np.array_equal(self.wire[a: a + fsz].cpu().numpy(), ref))
+            return bool(ok)
+        ids, desc, size = self.host
+        n = len(ids)
+        fsz = ca.frame_size(0x82, True, size)
+        ok = int(self.woff[-1].item()) == n * fsz
+        for q in (0, 1, n // 2, n - 1):
+            d = desc[q: q + 1].copy()
+            d["src_off"] = 0
+            ref, _ = oracle.encode_batch(wl_c5_payload(ids[q: q + 1], size), d)
+            ok &= bool(np.array_equal(self.wire[q * fsz: (q + 1) * fsz].cpu().numpy(), ref))
+        return bool(ok)
 
 
-def cpu_baseline(w, seconds):
-    """The oracle's faithful byte-loop restatement of the reference codec,
-    timed on this host on a bounded sample of the same workload."""
+def wl_c5_payload(ids, size):
+    from cppserver_amd import workloads as wl
+
+    return wl.c5_payload_np(ids, size)
+
+
+def cpu_baseline(w, seconds, cpu):
+    """The oracle's faithful byte-loop restatement of the reference codec
+    (ws.cpp:212-271 encode, :273-456 decode), timed on this host on a bounded
+    sample of the same workload: one thread, then `cpu["threads"]` threads
+    (one independent session per thread over a contiguous frame slice).
+    Returns (one, many) baseline dicts in the unit of the line's metric."""
     import oracle
 
-    if w.cfg != "c2":
-        return None, None
-    wire, fs, _ = w.host
-    n = len(fs)
-    per_frame = w.payload_bytes // n
-    # sample: the first m frames; size it so 1 thread runs ~seconds/2 in total
-    t_probe = oracle.time_decode(wire, fs[: max(1, n // 16)], threads=1, iters=1)
-    rate = (n // 16) * per_frame / max(t_probe, 1e-9)
-    m = n
-    iters = max(3, int((seconds / 2) * rate / (m * per_frame)))
-    fs_s = fs[:m]
-    t1 = oracle.time_decode(wire, fs_s, threads=1, iters=iters)
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    tn = oracle.time_decode(wire, fs_s, threads=threads, iters=max(3, iters * threads // 2))
-    sample = "%d frames x %d B (%.0f MiB), PrepareReceiveFrame per whole frame, median of %d passes" % (
-        m, per_frame, m * per_frame / 2**20, iters)
-    one = {"value": m * per_frame / t1 / GIB, "unit": "GiB/s", "cores": 1, "kind": "port", "sample": sample}
-    mt = {"value": m * per_frame / tn / GIB, "unit": "GiB/s", "cores": threads, "kind": "port",
-          "sample": sample + "; one session per thread over a contiguous frame slice"}
-    return one, mt
+    threads = cpu["threads"]
+
+    def pack(rate_1, rate_n, sample):
+        base = {"unit": "GiB/s", "kind": "port", "sample": sample, "cpu_model": cpu["cpu_model"],
+                "host_nproc": cpu["nproc"]}
+        return (dict(base, value=rate_1, cores=1),
+                dict(base, value=rate_n, cores=threads, sample=sample + "; one session per thread"))
+
+    if w.cfg == "c2":
+        wire, fs, _ = w.host
+        n = len(fs)
+        per_frame = w.payload_bytes // n
+        t_probe = oracle.time_decode(wire, fs[: max(1, n // 16)], threads=1, iters=1)
+        rate = (n // 16) * per_frame / max(t_probe, 1e-9)
+        iters = max(3, int((seconds / 2) * rate / (n * per_frame)))
+        t1 = oracle.time_decode(wire, fs, threads=1, iters=iters)
+        tn = oracle.time_decode(wire, fs, threads=threads, iters=max(3, iters * threads // 2))
+        sample = "%d frames x %d B (%.0f MiB), PrepareReceiveFrame per whole frame, median of %d passes" % (
+            n, per_frame, n * per_frame / 2**20, iters)
+        return pack(n * per_frame / t1 / GIB, n * per_frame / tn / GIB, sample)
+
+    def enc_sample(payload, desc, budget):
+        """First frames of the batch worth ~budget s of one-thread encode."""
+        probe = desc[: max(1, min(len(desc), 256))]
+        t = oracle.time_encode(payload, probe, threads=1, iters=1)
+        per = float(probe["len"].sum()) / max(t, 1e-9)
+        m, acc = 0, 0
+        cap = budget * per
+        while m < len(desc) and acc < cap:
+            acc += int(desc["len"][m])
+            m += 1
+        return desc[: max(1, m)]
+
+    if w.cfg == "c3":
+        payload, desc = w.host
+        sub = enc_sample(payload, desc, seconds / 4)
+        wire, off = oracle.encode_batch(payload, sub)
+        nb = float(sub["len"].sum())
+        e1 = oracle.time_encode(payload, sub, threads=1, iters=3)
+        d1 = oracle.time_decode(wire, off[:-1], threads=1, iters=3)
+        en = oracle.time_encode(payload, sub, threads=threads, iters=3)
+        dn = oracle.time_decode(wire, off[:-1], threads=threads, iters=3)
+        sample = ("first %d of the %d C3 frames (%.0f MiB payload), PrepareSendFrame then PrepareReceiveFrame per "
+                  "frame; rate = payload / (encode + decode time)" % (len(sub), len(desc), nb / 2**20))
+        return pack(nb / (e1 + d1) / GIB, nb / (en + dn) / GIB, sample)
+    if w.cfg == "c4":
+        payload, keys = w.host
+        k = len(keys)
+        desc = np.zeros(k, dtype=oracle_desc_dtype())
+        desc["len"] = w.length
+        desc["key"] = keys
+        desc["opcode"] = 0x82
+        desc["mask"] = 1
+        t1 = oracle.time_encode(payload, desc, threads=1, iters=5)
+        tn = oracle.time_encode(payload, desc, threads=threads, iters=5)
+        nb = float(k * w.length)
+        sample = ("one message: %d x PrepareSendFrame(0x82, mask, %d B) with the key set per call (the client "
+                  "path, SURVEY §3.3)" % (k, w.length))
+        return pack(nb / t1 / GIB, nb / tn / GIB, sample)
+    ids, desc, size = w.host
+    sub_n = max(1, min(len(ids), int(seconds / 4 * 0.5 * GIB / size)))
+    sub = desc[:sub_n].copy()
+    payload = wl_c5_payload(ids[:sub_n], size)
+    t1 = oracle.time_encode(payload, sub, threads=1, iters=3)
+    tn = oracle.time_encode(payload, sub, threads=threads, iters=3)
+    nb = float(sub_n * size)
+    sample = "first %d of the shard's %d C5 frames (%.0f MiB), PrepareSendFrame per frame" % (
+        sub_n, len(ids), nb / 2**20)
+    return pack(nb / t1 / GIB, nb / tn / GIB, sample)
+
+
+def oracle_desc_dtype():
+    from cppserver_amd.layout import SEND_DESC
+
+    return SEND_DESC
 
 
 def copy_ceiling(w, reps=10):
@@ -383,12 +543,12 @@ def fanout_graph_leg(w, per_graph=20, replays=10):
     c = w.codec
     wires = [w.wire, t.empty_like(w.wire)]
     for i in range(3):   # nothing is allocated inside a fan-out call; warm anyway
-        c.fanout(w.payload, w.keys, 0x82, True, wire=wires[i & 1])
+        c.fanout(w.payload, w.keys, 0x82, True, wire=wires[i & 1], length=w.length)
     t.cuda.synchronize()
     g = t.cuda.CUDAGraph()
     with t.cuda.graph(g):
         for i in range(per_graph):
-            c.fanout(w.payload, w.keys, 0x82, True, wire=wires[i & 1])
+            c.fanout(w.payload, w.keys, 0x82, True, wire=wires[i & 1], length=w.length)
     g.replay()
     t.cuda.synchronize()
     e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
@@ -402,10 +562,42 @@ def fanout_graph_leg(w, per_graph=20, replays=10):
             "GiBps": round(w.payload_bytes / (us * 1e-6) / GIB, 1)}
 
 
-def gather_leg(w, world, device):
+def _gather_tensors(wire, woff):
+    """Device tensors for RCCL; host copies when the group is gloo (the
+    $WSG_BENCH_BACKEND=gloo rehearsal of N ranks on fewer GPUs)."""
+    import torch.distributed as dist
+
+    if dist.get_backend() == "gloo":
+        n = int(woff[-1].item())
+        return wire[:n].cpu(), woff.cpu()
+    return wire, woff
+
+
+def gather_root_check(parts, n_total, size, chunk=1024):
+    """Root side of the C5 gather: reassemble the job in global frame order
+    and check sampled frames against the oracle (payload regenerated from
+    the frame index).  Returns (ok, job wire bytes)."""
+    import oracle
+    from cppserver_amd import shard
+    from cppserver_amd import workloads as wl
+
+    import cppserver_amd as ca
+
+    job, job_off = shard.reassemble(parts, n_total, chunk)
+    fsz = ca.frame_size(0x82, True, size)
+    ok = int(job_off[-1].item()) == n_total * fsz
+    for g in sorted({0, 1, chunk, n_total // 2 + 3, n_total - 1}):
+        ids = np.array([g])
+        ref, _ = oracle.encode_batch(wl.c5_payload_np(ids, size), wl.c5_desc(ids, size))
+        ok &= bool(np.array_equal(job[g * fsz: (g + 1) * fsz].cpu().numpy(), ref))
+    return bool(ok), int(job_off[-1].item())
+
+
+def gather_leg(w, world, rank, device):
     """C5's exchange step: every rank's framed output to rank 0 over RCCL
-    (variable-size grouped send/recv, cppserver_amd.shard.gather_frames),
-    timed once after the encode steps; reported beside the kernel rate."""
+    (torch.distributed's group: variable-size grouped send/recv,
+    cppserver_amd.shard.gather_frames), timed once after the encode steps
+    (max over ranks); the root reassembles and checks sampled frames."""
     import torch
 
     from cppserver_amd import shard
@@ -413,16 +605,103 @@ def gather_leg(w, world, device):
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
-    parts = shard.gather_frames(w.wire, w.woff)
+    parts = shard.gather_frames(*_gather_tensors(w.wire, w.woff))
     torch.cuda.synchronize()
-    barrier(world)
     dt = time.perf_counter() - t0
-    moved = None
+    barrier(world)
+    dt = max_over_ranks(dt, world, device)
+    res = {"ms": round(dt * 1e3, 3)}
     if parts is not None:
         moved = sum(int(p[1][-1].item()) for r, p in enumerate(parts) if r != 0)
-    dt = max_over_ranks(dt, world, device)
-    return {"ms": round(dt * 1e3, 3), "bytes_into_root": moved,
-            "GBps_into_root": round(moved / dt / 1e9, 1) if moved else None}
+        ids, desc, size = w.host
+        n_total = sum(int(p[1].numel()) - 1 for p in parts)
+        ok, total = gather_root_check(parts, n_total, size)
+        res.update({"bytes_into_root": moved, "GBps_into_root": round(moved / dt / 1e9, 1), "job_bytes": total,
+                    "root_check": ok})
+    return res
+
+
+def c5_job_leg(world, rank, device, codec, n_total=1 << 20, size=16384, chunk=1024):
+    """BASELINE config C5 beside the weak-scaling headline at N > 1: the 1 Mi x
+    16 KiB job dealt round-robin over the ranks (1024-frame chunks), every
+    rank encodes its shard on its GPU (wsg_encode_batch, payloads made in HBM),
+    and the framed output goes to rank 0 over RCCL (torch.distributed's
+    group); rank 0 reassembles the job in frame order and checks sampled
+    frames against the oracle.  Encode and gather times are max over ranks."""
+    import torch
+
+    import cppserver_amd as ca
+    from cppserver_amd import shard
+    from cppserver_amd import workloads as wl
+
+    ids = shard.rank_frames(rank, world, n_total, chunk)
+    payload = wl.c5_payload_torch(ids, size, device=device)
+    desc = ca.desc_to_tensor(wl.c5_desc(ids, size), device)
+    fsz = ca.frame_size(0x82, True, size)
+    wire = torch.empty(len(ids) * fsz, dtype=torch.uint8, device=device)
+    woff = torch.empty(len(ids) + 1, dtype=torch.int64, device=device)
+    codec.encode_batch(payload, desc, wire=wire, wire_cap=wire.numel(), wire_off=woff)   # warm
+    codec.sync()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world)
+    e0.record()
+    reps = 3
+    for _ in range(reps):
+        codec.encode_batch(payload, desc, wire=wire, wire_cap=wire.numel(), wire_off=woff)
+    e1.record()
+    e1.synchronize()
+    codec.sync()
+    enc_ms = max_over_ranks(e0.elapsed_time(e1) / reps, world, device)
+    del payload
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    parts = shard.gather_frames(*_gather_tensors(wire, woff))
+    torch.cuda.synchronize()
+    dt = max_over_ranks(time.perf_counter() - t0, world, device)
+    res = {"workload": "C5: %d x %d B frames round-robin (chunks of %d) over %d GPUs, gather to rank 0"
+                       % (n_total, size, chunk, world),
+           "encode_ms": round(enc_ms, 3),
+           "encode_GiBps_job": round(n_total * size / (enc_ms * 1e-3) / GIB, 1),
+           "gather_ms": round(dt * 1e3, 3)}
+    if parts is not None:
+        moved = sum(int(p[1][-1].item()) for r, p in enumerate(parts) if r != 0)
+        ok, total = gather_root_check(parts, n_total, size, chunk)
+        res.update({"bytes_into_root": moved, "GBps_into_root": round(moved / dt / 1e9, 1), "job_bytes": total,
+                    "root_check": ok})
+    del parts, wire
+    torch.cuda.empty_cache()
+    return res
+
+
+def fanout_many_leg(w, m=16, reps=10):
+    """The multicast tick (ws_multicast_server.cpp:104-114: `messages_rate`
+    messages per tick, each to every client) as ONE wsg_fanout_encode_many
+    call: m x C4 (4 KiB messages x 10000 client keys, 41 MB of frames each),
+    timed back to back; per-message time next to the single fan-out step."""
+    t = w.torch
+    c = w.codec
+    rng = np.random.default_rng(99)
+    length, k = w.length, int(w.keys.numel())
+    arena = t.from_numpy(rng.integers(0, 256, m * length, dtype=np.uint8)).to(w.keys.device)
+    src = np.arange(m, dtype=np.uint64) * np.uint64(length)
+    lens = np.full(m, length, dtype=np.uint64)
+    ops = np.full(m, 0x82, dtype=np.uint8)
+    wire, off = c.fanout_many(arena, src, lens, ops, w.keys)
+    c.sync()
+    e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        c.fanout_many(arena, src, lens, ops, w.keys, wire=wire)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    import cppserver_amd as ca
+
+    fsz = ca.frame_size(0x82, True, length)
+    bytes_out = m * k * fsz
+    return {"messages": m, "us_per_call": round(ms * 1e3, 2), "us_per_message": round(ms * 1e3 / m, 2),
+            "write_GBps": round(bytes_out / (ms * 1e-3) / 1e9, 1), "frame_bytes": fsz}
 
 
 def main():
@@ -476,18 +755,28 @@ def main():
     k_avg_ms = kernel_ms / max(launches, 1)
     k_avg_ms = max_over_ranks(k_avg_ms, world, device)
     achieved = w.alg_bytes / (k_avg_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(args.pmc, w.cfg) if args.frames is None and args.size is None else None
+    pmc_key = w.cfg + ("x%d" % w.m if w.cfg == "c4" and w.m > 1 else "")
+    traffic = pmc_traffic(args.pmc, pmc_key) if args.frames is None and args.size is None else None
 
     extras = {}
     if w.cfg == "c5" and world > 1:
-        extras["gather"] = gather_leg(w, world, device)
+        extras["gather"] = gather_leg(w, world, rank, device)
+    if w.cfg == "c2" and world > 1 and not args.no_c5_job:
+        # C5 (BASELINE configs[4]) on the same GPUs: a failure here is reported
+        # in the line, it does not take the headline with it
+        try:
+            extras["c5_job"] = c5_job_leg(world, rank, device, codec,
+                                          n_total=int(os.environ.get("WSG_C5_FRAMES", 1 << 20)))
+        except Exception as e:   # noqa: BLE001
+            extras["c5_job"] = {"error": repr(e)[:300]}
     if rank == 0 and world == 1 and not args.no_extras:
         extras["copy_ceiling_GBps"] = round(copy_ceiling(w), 1)
         pc = pcie_inclusive(w)
         if pc is not None:
             extras["pcie_inclusive_GiBps"] = pc
-        if w.cfg == "c4":
+        if w.cfg == "c4" and w.m == 1:
             extras["hip_graph"] = fanout_graph_leg(w)
+            extras["fanout_many"] = fanout_many_leg(w)
         if w.cfg == "c2":
             extras["echo_size_device"] = echo_size_leg(w)
             sb = session_batch_leg()
@@ -495,7 +784,7 @@ def main():
                 extras["session_batch"] = sb
     cpu1 = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu1, cpu_mt = cpu_baseline(w, args.cpu_seconds)
+        cpu1, cpu_mt = cpu_baseline(w, args.cpu_seconds, host_cpu())
 
     if world > 1:
         import torch.distributed as dist

@@ -60,6 +60,7 @@ def lib(path=None):
         "wsg_decode_batch": (ci, [vp, vp, u64, vp, u32, vp, vp, vp]),
         "wsg_encode_batch": (ci, [vp, vp, vp, u32, vp, u64, vp, vp]),
         "wsg_fanout_encode": (ci, [vp, vp, u64, vp, u32, ctypes.c_uint8, ci, vp, u64, vp]),
+        "wsg_fanout_encode_many": (ci, [vp, vp, vp, vp, vp, u32, vp, u32, ci, vp, u64, vp, vp]),
         "wsg_xor_host": (ci, [vp, vp, vp, sz, u32, u32]),
         "wsg_decode_batch_host": (ci, [vp, vp, u64, vp, u32, vp, vp]),
         "wsg_encode_batch_host": (ci, [vp, vp, u64, vp, u32, vp, u64, vp]),
@@ -89,6 +90,14 @@ def lib(path=None):
         "wsg_tx_forget": (ci, [vp, vp]),
         "wsg_tx_pending": (ci, [vp, ctypes.POINTER(u32), ctypes.POINTER(u64)]),
         "wsg_tx_flush": (ci, [vp, vp, vp, ctypes.POINTER(u32)]),
+        "wsg_mgpu_create": (ci, [vp, ci, ctypes.POINTER(vp)]),
+        "wsg_mgpu_unique_id": (ci, [vp]),
+        "wsg_mgpu_create_rank": (ci, [ci, vp, ci, ci, ctypes.POINTER(vp)]),
+        "wsg_mgpu_destroy": (ci, [vp]),
+        "wsg_mgpu_info": (ci, [vp, ctypes.POINTER(ci), ctypes.POINTER(ci), ctypes.POINTER(ci)]),
+        "wsg_mgpu_ctx": (vp, [vp, ci]),
+        "wsg_mgpu_shard_count": (u64, [u64, u32, ci, ci]),
+        "wsg_mgpu_encode_gather": (ci, [vp, u64, u32, vp, vp, vp, vp, vp, vp, ci, vp, u64, vp, vp]),
         "wsg_timing_enable": (ci, [vp, ci]),
         "wsg_timing_read": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ci]),
     }
@@ -237,6 +246,28 @@ class Codec:
                                        ctypes.c_void_p(wire.data_ptr()), wire.numel(), self._stream(stream))
         _check(rc, "wsg_fanout_encode")
         return wire
+
+    def fanout_many(self, payload, src_off, lens, opcodes, keys, mask=True, wire=None, stream=None):
+        """m messages (payload[src_off[i]:][:lens[i]], opcode opcodes[i]) x k
+        keys in one call (wsg_fanout_encode_many).  Returns (wire, wire_off):
+        message i's k frames start at wire_off[i] (host numpy, m + 1)."""
+        t = self._torch
+        src_off = np.ascontiguousarray(src_off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        opcodes = np.ascontiguousarray(opcodes, dtype=np.uint8)
+        m, k = len(lens), int(keys.numel())
+        need = 0
+        for i in range(m):
+            need = (need + 127) // 128 * 128 + frame_size(int(opcodes[i]), mask, int(lens[i])) * k
+        if wire is None:
+            wire = t.empty(max(need, 16), dtype=t.uint8, device=keys.device)
+        off = np.zeros(m + 1, dtype=np.uint64)
+        rc = self._L.wsg_fanout_encode_many(self._ctx, ctypes.c_void_p(payload.data_ptr()), _np_ptr(src_off),
+                                            _np_ptr(lens), _np_ptr(opcodes), m, ctypes.c_void_p(keys.data_ptr()), k,
+                                            1 if mask else 0, ctypes.c_void_p(wire.data_ptr()), wire.numel(),
+                                            _np_ptr(off), self._stream(stream))
+        _check(rc, "wsg_fanout_encode_many")
+        return wire, off
 
     # -- host-staged paths ----------------------------------------------------
     def xor_host(self, data, key, phase=0):
@@ -462,3 +493,74 @@ def desc_to_tensor(desc, device):
 
     desc = np.ascontiguousarray(desc, dtype=SEND_DESC)
     return torch.from_numpy(desc.view(np.uint8).copy()).to(device)
+
+
+def _ptr_array(ptrs):
+    return (ctypes.c_void_p * len(ptrs))(*[ctypes.c_void_p(p) for p in ptrs])
+
+
+class MultiGPU:
+    """The multi-GPU entry of the C-ABI (wsg_mgpu_*): round-robin shards of a
+    frame batch encoded on their GPUs and gathered to one rank over RCCL.
+
+    MultiGPU(devices=[0, 1, ...]) drives several GPUs from this process;
+    MultiGPU.rank(device, uid, rank, world) is one rank of a multi-process
+    group (uid from MultiGPU.unique_id() on rank 0, handed to every rank)."""
+
+    ID_BYTES = 128
+
+    def __init__(self, devices=None, _handle=None):
+        self._L = lib()
+        if _handle is not None:
+            self._g = _handle
+        else:
+            devs = (ctypes.c_int * len(devices))(*devices)
+            g = ctypes.c_void_p()
+            _check(self._L.wsg_mgpu_create(devs, len(devices), ctypes.byref(g)), "wsg_mgpu_create")
+            self._g = g
+        w, nl, fr = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(self._L.wsg_mgpu_info(self._g, ctypes.byref(w), ctypes.byref(nl), ctypes.byref(fr)), "wsg_mgpu_info")
+        self.world, self.nlocal, self.first_rank = w.value, nl.value, fr.value
+
+    @staticmethod
+    def unique_id():
+        buf = (ctypes.c_uint8 * MultiGPU.ID_BYTES)()
+        _check(lib().wsg_mgpu_unique_id(buf), "wsg_mgpu_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def rank(cls, device, uid, rank, world):
+        g = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * cls.ID_BYTES).from_buffer_copy(bytes(uid))
+        _check(lib().wsg_mgpu_create_rank(device, buf, rank, world, ctypes.byref(g)), "wsg_mgpu_create_rank")
+        return cls(_handle=g)
+
+    @staticmethod
+    def shard_count(n_total, chunk, world, rank):
+        return int(lib().wsg_mgpu_shard_count(n_total, chunk, world, rank))
+
+    def close(self):
+        if getattr(self, "_g", None):
+            self._L.wsg_mgpu_destroy(self._g)
+            self._g = None
+
+    __del__ = close
+
+    def encode_gather(self, n_total, chunk, payloads, descs, wires, wire_offs, root=0, out=None, out_off=None):
+        """Per local rank (lists of CUDA tensors): payload arena, descriptor
+        bytes (n_local * 32), wire buffer, wire_off (n_local + 1 int64).  On
+        the root: `out` (uint8) and `out_off` (int64, n_total + 1, or None).
+        Returns (encode_ms, gather_ms)."""
+        k = self.nlocal
+        n_local = (ctypes.c_uint32 * k)(*[int(d.numel()) // SEND_DESC.itemsize for d in descs])
+        caps = (ctypes.c_uint64 * k)(*[int(w.numel()) for w in wires])
+        times = (ctypes.c_double * 2)()
+        rc = self._L.wsg_mgpu_encode_gather(
+            self._g, int(n_total), int(chunk), _ptr_array([p.data_ptr() for p in payloads]),
+            _ptr_array([d.data_ptr() for d in descs]), n_local, _ptr_array([w.data_ptr() for w in wires]), caps,
+            _ptr_array([o.data_ptr() for o in wire_offs]), int(root),
+            ctypes.c_void_p(out.data_ptr() if out is not None else 0), int(out.numel()) if out is not None else 0,
+            ctypes.c_void_p(out_off.data_ptr() if out_off is not None else 0), times)
+        _check(rc, "wsg_mgpu_encode_gather")
+        return times[0], times[1]
+

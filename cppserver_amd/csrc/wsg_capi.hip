@@ -454,6 +454,68 @@ int wsg_encode_batch(wsg_ctx* c, const uint8_t* d_payload, const wsg_send_desc* 
     return encode_launch(c, s, d_payload, d_desc, n, d_wire, wire_cap, d_wire_off, c->enc);
 }
 
+namespace {
+
+// One fan-out message's k frames on the flat / piece kernels (frame sizes the
+// period path does not take).
+int fanout_one_flat(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, uint64_t len, const uint32_t* d_keys,
+                    uint32_t k, uint8_t opcode, int mask, uint8_t* d_wire)
+{
+    const uint64_t fsize = wsg_frame_size(opcode, mask, len, 0);
+    const uint64_t total = fsize * k;
+    const uint64_t pieces = uint64_t(k) * ((fsize + wsg::PIECE_ALIGN - 1 + wsg::PIECE - 1) / wsg::PIECE);
+    const uint64_t blocks = wsg::fanout_flat ? ceil_div(ceil_div(total, wsg::CHUNK), wsg::BLOCK * wsg::FAN_UNITS)
+                                             : ceil_div(pieces, wsg::BLOCK / 64);
+    WSG_HIP(wsg::launch_fanout(s, grid_for(c, blocks), d_payload, len, d_keys, k, opcode, mask ? 1u : 0u, fsize,
+                               d_wire));
+    return WSG_OK;
+}
+
+// m messages x k keys.  Messages of one geometry (length, opcode) whose frame
+// size suits the period kernel go FAN_MSGS at a time into one launch
+// (blockIdx.y = message); the others take one flat launch each.
+int fanout_many(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, const uint64_t* src_off, const uint64_t* len,
+                const uint8_t* opcode, uint32_t m, const uint32_t* d_keys, uint32_t k, int mask, uint8_t* d_wire,
+                const uint64_t* wire_off)
+{
+    std::vector<char> done(m, 0);
+    for (uint32_t i = 0; i < m; ++i) {
+        if (done[i])
+            continue;
+        const uint64_t fsize = wsg_frame_size(opcode[i], mask, len[i], 0);
+        wsg::FanMsgs g{};
+        uint32_t cnt = 0;
+        std::vector<uint32_t> members;
+        for (uint32_t q = i; q < m; ++q) {
+            if (done[q] || len[q] != len[i] || opcode[q] != opcode[i])
+                continue;
+            members.push_back(q);
+        }
+        for (size_t at = 0; at < members.size(); at += wsg::FAN_MSGS) {
+            cnt = uint32_t(std::min<size_t>(wsg::FAN_MSGS, members.size() - at));
+            for (uint32_t q = 0; q < cnt; ++q) {
+                g.src[q] = src_off[members[at + q]];
+                g.dst[q] = wire_off[members[at + q]];
+            }
+            hipError_t perr = hipSuccess;
+            if (wsg::launch_fanout_period(s, c->num_cus, c->fan_waves_per_cu, d_payload, len[i], d_keys, k, opcode[i],
+                                          mask ? 1u : 0u, fsize, d_wire, g, cnt, &perr)) {
+                WSG_HIP(perr);
+            } else {
+                for (uint32_t q = 0; q < cnt; ++q)
+                    if (int rc = fanout_one_flat(c, s, d_payload + g.src[q], len[i], d_keys, k, opcode[i], mask,
+                                                 d_wire + g.dst[q]))
+                        return rc;
+            }
+        }
+        for (uint32_t q : members)
+            done[q] = 1;
+    }
+    return WSG_OK;
+}
+
+} // namespace
+
 int wsg_fanout_encode(wsg_ctx* c, const uint8_t* d_payload, uint64_t len, const uint32_t* d_keys, uint32_t k,
                       uint8_t opcode, int mask, uint8_t* d_wire, uint64_t wire_cap, void* stream)
 {
@@ -463,24 +525,46 @@ int wsg_fanout_encode(wsg_ctx* c, const uint8_t* d_payload, uint64_t len, const 
         return WSG_EINVAL;
     if (k == 0)
         return WSG_OK;
-    const uint64_t fsize = wsg_frame_size(opcode, mask, len, 0);
-    const uint64_t total = fsize * k;
+    const uint64_t total = wsg_frame_size(opcode, mask, len, 0) * k;
     if (total > wire_cap)
         return WSG_ENOMEM;
     hipStream_t s = pick(c, stream);
+    const uint64_t src = 0, off[2] = {0, total};
     const int t = timing_begin(c, s);
-    hipError_t perr = hipSuccess;
-    if (wsg::launch_fanout_period(s, c->num_cus, c->fan_waves_per_cu, d_payload, len, d_keys, k, opcode, mask ? 1u : 0u,
-                                  fsize, d_wire, &perr)) {
-        WSG_HIP(perr);
-        timing_end(c, s, t);
-        return WSG_OK;
+    if (int rc = fanout_many(c, s, d_payload, &src, &len, &opcode, 1, d_keys, k, mask, d_wire, off))
+        return rc;
+    timing_end(c, s, t);
+    return WSG_OK;
+}
+
+int wsg_fanout_encode_many(wsg_ctx* c, const uint8_t* d_payload, const uint64_t* src_off, const uint64_t* len,
+                           const uint8_t* opcode, uint32_t m, const uint32_t* d_keys, uint32_t k, int mask,
+                           uint8_t* d_wire, uint64_t wire_cap, uint64_t* wire_off, void* stream)
+{
+    if (!c || !wire_off || (m && (!src_off || !len || !opcode)) || (m && k && (!d_keys || !d_wire)))
+        return WSG_EINVAL;
+    if (d_wire && !aligned16(d_wire))
+        return WSG_EINVAL;
+    // message i's frames from wire_off[i], line-aligned (whole-line store rows)
+    uint64_t at = 0;
+    bool any_payload = false;
+    for (uint32_t i = 0; i < m; ++i) {
+        at = (at + wsg::PIECE_ALIGN - 1) & ~(wsg::PIECE_ALIGN - 1);
+        wire_off[i] = at;
+        at += wsg_frame_size(opcode[i], mask, len[i], 0) * k;
+        any_payload = any_payload || len[i] != 0;
     }
-    const uint64_t pieces = uint64_t(k) * ((fsize + wsg::PIECE_ALIGN - 1 + wsg::PIECE - 1) / wsg::PIECE);
-    const uint64_t blocks = wsg::fanout_flat ? ceil_div(ceil_div(total, wsg::CHUNK), wsg::BLOCK * wsg::FAN_UNITS)
-                                             : ceil_div(pieces, wsg::BLOCK / 64);
-    WSG_HIP(wsg::launch_fanout(s, grid_for(c, blocks), d_payload, len, d_keys, k, opcode, mask ? 1u : 0u, fsize,
-                               d_wire));
+    wire_off[m] = at;
+    if (at > wire_cap)
+        return WSG_ENOMEM;
+    if (m == 0 || k == 0)
+        return WSG_OK;
+    if (any_payload && !d_payload)
+        return WSG_EINVAL;
+    hipStream_t s = pick(c, stream);
+    const int t = timing_begin(c, s);
+    if (int rc = fanout_many(c, s, d_payload, src_off, len, opcode, m, d_keys, k, mask, d_wire, wire_off))
+        return rc;
     timing_end(c, s, t);
     return WSG_OK;
 }

@@ -69,12 +69,24 @@ hipError_t launch_encode_scan_small(hipStream_t s, const wsg_send_desc* desc, ui
 hipError_t launch_encode_small(hipStream_t s, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
                                uint64_t* wire_off, const uint64_t* scan, uint8_t* wire, uint64_t wire_cap,
                                unsigned long long* err);
+// Messages of one fan-out launch (blockIdx.y): payload and output offsets.
+constexpr int FAN_MSGS = 32;
+struct FanMsgs {
+    uint64_t src[FAN_MSGS];   // message payload offset from the payload base
+    uint64_t dst[FAN_MSGS];   // wire offset of the message's first frame
+};
+// Period-path fan-out of nmsgs (<= FAN_MSGS) messages of one geometry; false:
+// the frame size does not suit it (the caller takes launch_fanout per message).
 bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_t* payload, uint64_t len,
                           const uint32_t* keys, uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize,
-                          uint8_t* wire, hipError_t* err);
+                          uint8_t* wire, const FanMsgs& msgs, uint32_t nmsgs, hipError_t* err);
 hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64_t len, const uint32_t* keys,
                          uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire);
 hipError_t launch_xor(hipStream_t s, int grid, const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,
                       uint32_t phase);
+// Multi-GPU gather (wsg_mgpu.cpp): out_off[g] = stage[g] - stage[first frame of
+// g's chunk] + goff[chunk]; out_off[n_total] = total.
+hipError_t launch_rebase_offsets(hipStream_t s, const uint64_t* stage, const uint64_t* goff, uint64_t n_total,
+                                 uint32_t chunk, uint64_t* out_off, uint64_t total);
 
 } // namespace wsg

@@ -59,6 +59,9 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_DEC_WAVES
 #define WSG_DEC_WAVES 1   // k_decode minimum waves/SIMD (register cap); 6 and 8 spill and run slower
 #endif
+#ifndef WSG_DEC_RELOAD
+#define WSG_DEC_RELOAD 1   // k_decode staged tiles re-read their bytes instead of holding them in registers
+#endif
 #ifndef WSG_FAN_PERIOD
 #define WSG_FAN_PERIOD 1   // fan-out: period path (k_fanout_period) where the frame size allows; 0 = flat kernel only
 #endif
@@ -82,6 +85,38 @@ __device__ __forceinline__ void st16nt(uint8_t* p, v4u v)
     else
         *reinterpret_cast<v4u*>(p) = v;
 }
+
+// Stores of a once-written output stream.  Write-through (sc1) buffer stores
+// beat nontemporal ones in tools/membench.hip's copy (C2 footprint: 83.8-83.9
+// vs 85.0-85.5 us) and write-only stream (43.6 vs 47.4 us), but NOT in
+// k_decode: 90.7 vs 87.9 us on C2 and 0.825 vs 0.782 ms on C3's ragged
+// frames (tools/tune.py, same box, interleaved), so decode keeps nontemporal
+// stores; WSG_OUT_SC1=1 builds the write-through variant for A/B runs.
+#ifndef WSG_OUT_SC1
+#define WSG_OUT_SC1 0
+#endif
+#ifndef WSG_FAN_SC1
+#define WSG_FAN_SC1 0   // fan-out period path: write-through stores (A/B)
+#endif
+struct OutTile {
+    uint8_t* p;   // tile base (wave-uniform)
+    bool sc1;
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ OutTile(uint8_t* base, uint32_t bytes, bool write_through = WSG_OUT_SC1 != 0)
+        : p(base), sc1(write_through)
+    {
+        if (sc1)
+            rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
+    }
+    // whole 16-B chunk at tile offset o (o + 16 <= bytes)
+    __device__ __forceinline__ void put(uint32_t o, v4u v) const
+    {
+        if (sc1)
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, o, 0, 16);
+        else
+            st16nt(p + o, v);
+    }
+};
 
 __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t b)
 {
@@ -140,12 +175,6 @@ __device__ __forceinline__ void put_byte(v4u& w, uint32_t j, uint32_t b)
     w.y |= uint32_t(lo >> 32);
     w.z |= uint32_t(hi);
     w.w |= uint32_t(hi >> 32);
-}
-
-__device__ __forceinline__ void store_partial(uint8_t* dst, v4u w, uint32_t nbytes)
-{
-    for (uint32_t j = 0; j < nbytes; ++j)
-        dst[j] = uint8_t(lane_byte(w, j));
 }
 
 #ifndef WSG_STAGE_FPL
@@ -293,6 +322,22 @@ __device__ __forceinline__ int frame_parse(const uint8_t* __restrict__ wire, uin
     return e;
 }
 
+// wsg_recv_info as four 8-byte words (a struct store of the byte fields went
+// through scratch).
+__device__ __forceinline__ void store_info(wsg_recv_info* dst, const wsg_recv_info& r)
+{
+    static_assert(offsetof(wsg_recv_info, key) == 16 && offsetof(wsg_recv_info, opcode) == 20 &&
+                      offsetof(wsg_recv_info, b0) == 24 && offsetof(wsg_recv_info, error) == 25 &&
+                      sizeof(wsg_recv_info) == 32,
+                  "wsg_recv_info layout");
+    uint64_t* w = reinterpret_cast<uint64_t*>(dst);
+    w[0] = r.payload_off;
+    w[1] = r.len;
+    w[2] = uint64_t(r.key) | (uint64_t(r.opcode) << 32) | (uint64_t(r.fin) << 40) | (uint64_t(r.masked) << 48) |
+           (uint64_t(r.hdr_len) << 56);
+    w[3] = uint64_t(r.b0) | (uint64_t(uint8_t(r.error)) << 8);
+}
+
 __device__ __forceinline__ uint64_t fs_at(const uint64_t* __restrict__ fs, uint32_t n, int64_t i)
 {
     return fs[min<int64_t>(i, int64_t(n) - 1)];   // clamped: the load never depends on a compare
@@ -386,15 +431,6 @@ __device__ __forceinline__ void locate(const uint64_t* __restrict__ fs, uint32_t
     }
 }
 
-// Store chunk [p, p + 16) of a tile ending at tend (partial at the wire's end).
-__device__ __forceinline__ void store_chunk(uint8_t* out, uint64_t p, uint64_t tend, v4u w)
-{
-    if (p + CHUNK <= tend)
-        st16nt(out + p, w);
-    else if (p < tend)
-        store_partial(out + p, w, uint32_t(tend - p));
-}
-
 // A frame's payload as seen from one tile: bytes [lo, hi) of the tile
 // (tile-relative, clamped to the tile; for the frames of a tile in order,
 // lo and hi are non-decreasing) XOR with kr, the frame's key rotated
@@ -454,7 +490,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
             const int e = frame_parse(wire, wire_len, fs[i], i + 1 < n ? fs[i + 1] : wire_len, r);
             if (e != 0)
                 atomicMin(err, (static_cast<unsigned long long>(i) << 8) | static_cast<unsigned long long>(-e));
-            info[i] = r;
+            store_info(info + i, r);
         }
     }
 
@@ -478,9 +514,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
             for (int u = 0; u < UNROLL; ++u)
                 v[u] = ld16nt(wire + base + lane_off(u));
         } else {
+            // the wire's last, partial tile always takes the staged path,
+            // which reads its bytes itself (never past the wire's end)
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u)
-                v[u] = (lane_off(u) < span) ? ld16(wire + base + lane_off(u)) : v4u{0, 0, 0, 0};
+                v[u] = v4u{0, 0, 0, 0};
         }
 
         TileLoc L;
@@ -515,11 +553,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
             if (S[0].lo == 0 && S[0].hi == TILE) {
 #endif
                 // stream: the whole tile is payload of one frame
+                const OutTile ot(out + base, uint32_t(TILE));
 #pragma unroll
                 for (int u = 0; u < UNROLL; ++u)
-                    st16nt(out + base + lane_off(u), v[u] ^ S[0].kr);
+                    ot.put(uint32_t(lane_off(u)), v[u] ^ S[0].kr);
                 continue;
             }
+            const OutTile ot(out + base, uint32_t(TILE));
             // boundary: per chunk, the key word of the segment holding it;
             // the few chunks a segment edge cuts build byte masks
 #pragma unroll
@@ -539,13 +579,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
                     for (int k = 1; k < MAXF; ++k)
                         x |= seg_xor(o, S[k]);
                 }
-                st16nt(out + base + o, v[u] ^ x);
+                ot.put(o, v[u] ^ x);
             }
             continue;
         }
 
         // staged: payload segments in LDS, LDSF frames per round
         __shared__ uint32_t s_lo[LDSF], s_hi[LDSF], s_kr[LDSF];
+        __shared__ uint32_t s_wcnt[BLOCK / 64];
         // stage the segments of frames r0, r0 + 1, ... that touch the tile;
         // more = frames past the stage touch it too (block-uniform)
         auto stage = [&](uint64_t r0, int& cnt, bool& more) {
@@ -564,13 +605,27 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
                 // frame `first` touches (c > MAXF); the others when they start in the tile
                 touch[q] = fi < n && (fi == L.first || sj[q] < tend);
             }
-            __syncthreads();   // the previous readers are done with the stage
-            cnt = 0;
+            // block-wide counts from wave ballots through LDS (the
+            // __syncthreads_count / _or builtins cost ~40 VGPRs here,
+            // tools/regs.py: 91 vs 53 for the whole kernel)
+            uint32_t wc = 0;
 #pragma unroll
             for (int q = 0; q < SPL; ++q)
-                cnt += __syncthreads_count(touch[q]);
-            more = __syncthreads_or(threadIdx.x == BLOCK - 1 && touch[SPL - 1] &&
-                                    r0 + uint64_t(LDSF) < n && lim[SPL - 1] < tend);
+                wc += uint32_t(__builtin_popcountll(__ballot(touch[q])));
+            const bool last_more = __ballot(threadIdx.x == BLOCK - 1 && touch[SPL - 1] &&
+                                            r0 + uint64_t(LDSF) < n && lim[SPL - 1] < tend) != 0;
+            __syncthreads();   // the previous readers are done with the stage and the counts
+            if ((threadIdx.x & 63) == 0)
+                s_wcnt[threadIdx.x >> 6] = wc | (last_more ? 0x80000000u : 0u);
+            __syncthreads();
+            cnt = 0;
+            more = false;
+#pragma unroll
+            for (int w = 0; w < BLOCK / 64; ++w) {
+                const uint32_t x = s_wcnt[w];
+                cnt += int(x & 0x7FFFFFFFu);
+                more = more || (x >> 31) != 0;
+            }
 #pragma unroll 1
             for (int q = 0; q < SPL; ++q) {
                 const int slot = q * BLOCK + int(threadIdx.x);
@@ -602,49 +657,43 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
                 x |= seg_xor(o, Seg{s_lo[j], s_hi[j], s_kr[j]});
             return x;
         };
-        // rounds of LDSF frames; one round (the common case) stores straight
-        // from registers, more rounds (tiny frames) accumulate each thread's
-        // XOR words in its own LDS slots (a register array carried around
-        // the round loop would cost occupancy)
+        // rounds of LDSF frames (one for every tile but those of the tiniest
+        // frames): each round ORs its segments' XOR words into the thread's
+        // own LDS slots, then one pass reads the tile's bytes again (L2 /
+        // Infinity-Cache warm), XORs and stores.  Nothing is carried in
+        // registers across the staging: this path would otherwise set the
+        // kernel's register budget (95 VGPRs with the tile held in registers
+        // and a per-round store, 5 waves/SIMD; tools/regs.py).
         __shared__ v4u s_acc[UNROLL][BLOCK];
+#pragma unroll 1
         for (uint64_t r0 = L.first;; r0 += LDSF) {
             int cnt;
             bool more;
             stage(r0, cnt, more);
-            if (r0 == L.first && !more) {
-                // whole chunks stored as they are built; the one chunk the
-                // wire's end cuts (if any) afterwards: one byte loop
-                v4u tail_w = {0, 0, 0, 0};
-                uint64_t tail_p = ~uint64_t(0);
-#pragma unroll
-                for (int u = 0; u < UNROLL; ++u) {
-                    const uint64_t p = base + lane_off(u);
-                    const v4u w = v[u] ^ chunk_xor(uint32_t(lane_off(u)), cnt);
-                    if (p + CHUNK <= tend) {
-                        st16nt(out + p, w);
-                    } else if (p < tend) {
-                        tail_w = w;
-                        tail_p = p;
-                    }
-                }
-                if (tail_p != ~uint64_t(0))
-                    store_partial(out + tail_p, tail_w, uint32_t(tend - tail_p));
-                break;
-            }
 #pragma unroll 1
             for (int u = 0; u < UNROLL; ++u) {
                 const v4u x = chunk_xor(uint32_t(lane_off(u)), cnt);
                 s_acc[u][threadIdx.x] = (r0 == L.first) ? x : (s_acc[u][threadIdx.x] | x);
             }
-            if (more)
-                continue;
+            if (!more)
+                break;
+        }
+        {
+            const OutTile ot(out + base, uint32_t(TILE));
 #pragma unroll 1
             for (int u = 0; u < UNROLL; ++u) {
-                const uint64_t p = base + lane_off(u);
-                const v4u d = p < tend ? ld16(wire + p) : v4u{0, 0, 0, 0};
-                store_chunk(out, p, tend, d ^ s_acc[u][threadIdx.x]);
+                const uint32_t o = uint32_t(lane_off(u));
+                if (o + CHUNK <= span) {
+                    ot.put(o, ld16(wire + base + o) ^ s_acc[u][threadIdx.x]);
+                } else if (o < span) {
+                    // the chunk the wire's end cuts: bytes only, through the
+                    // thread's LDS slot (no register byte shuffles)
+                    uint8_t* b = reinterpret_cast<uint8_t*>(&s_acc[u][threadIdx.x]);
+#pragma unroll 1
+                    for (uint32_t k = 0; k < span - o; ++k)
+                        out[base + o + k] = uint8_t(wire[base + o + k] ^ b[k]);
+                }
             }
-            break;
         }
     }
 }
@@ -1423,13 +1472,20 @@ __global__ __launch_bounds__(BLOCK) void k_fanout_flat(const uint8_t* __restrict
 // The wave's keys for all its passes come in one vector load up front (lane
 // q holds key P * (first group of pass q / 2P) + q % 2P) and are picked per
 // pass with a lane shuffle.  Rows are 1 KiB-aligned, whole lines per wave.
+//
+// Many messages in one launch (wsg_fanout_encode_many, the ws_multicast tick):
+// blockIdx.y picks message y of up to FAN_MSGS messages of one geometry
+// (length, opcode), whose payload and output start come from the kernel
+// arguments; the k frames of every message are written exactly as for one.
 template <int P>
-__global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict__ payload, uint64_t len,
+__global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict__ payload0, uint64_t len,
                                                       const uint32_t* __restrict__ keys, uint32_t k, uint8_t opcode,
                                                       uint32_t mask, uint64_t fsize, uint32_t G, uint32_t dm,
-                                                      uint8_t* __restrict__ wire)
+                                                      uint8_t* __restrict__ wire0, const FanMsgs msgs)
 {
     constexpr int KW = 2 * P;   // keys per pass: the row spans <= 2 groups (G >= 64)
+    const uint8_t* __restrict__ payload = payload0 + msgs.src[blockIdx.y];
+    uint8_t* __restrict__ wire = wire0 + msgs.dst[blockIdx.y];
     const FanGeom f = fan_geom(opcode, mask != 0, len);
     const uint64_t total = fsize * k;
     const uint64_t chunks = (total + CHUNK - 1) / CHUNK;
@@ -1483,8 +1539,14 @@ __global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict_
         const uint32_t kb = __builtin_amdgcn_ds_bpermute(int(sb + (ia + 1) * 4), int(kreg));
         const uint32_t ra = key_rot(ka, pa), rb = key_rot(kb, pb);
         const v4u w = t ^ (ma & v4u{ra, ra, ra, ra}) ^ (mb & v4u{rb, rb, rb, rb});
-        if (c < chunks)
+        if (WSG_FAN_SC1 && c + 1 < chunks) {
+            // write-through store of a whole chunk (resource at the pass row)
+            const uint64_t row = row0 + uint64_t(it) * rstep;
+            const OutTile ot(wire + row * CHUNK, 64 * CHUNK, true);
+            ot.put(lane * CHUNK, w);
+        } else if (c < chunks) {
             fan_store(wire, c, chunks, total, w);
+        }
     }
 }
 
@@ -1594,8 +1656,10 @@ hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64
 // passes per wave that one key load covers them (passes * 2P <= 64 * WSG_FAN_KV).
 bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_t* payload, uint64_t len,
                           const uint32_t* keys, uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize,
-                          uint8_t* wire, hipError_t* err)
+                          uint8_t* wire, const FanMsgs& msgs, uint32_t nmsgs, hipError_t* err)
 {
+    if (nmsgs == 0 || nmsgs > uint32_t(FAN_MSGS))
+        return false;
     if (!WSG_FAN_PERIOD || fsize % 4 != 0)
         return false;
     uint64_t g16 = 16;
@@ -1624,17 +1688,41 @@ bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_
     const uint64_t wpb = 1;   // waves per block: one (4-wave blocks measured 8 % slower at C4)
     switch (P) {
     case 1:
-        k_fanout_period<1><<<uint32_t(W / wpb), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire);
+        k_fanout_period<1><<<dim3(uint32_t(W / wpb), nmsgs), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire, msgs);
         break;
     case 2:
-        k_fanout_period<2><<<uint32_t(W / wpb), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire);
+        k_fanout_period<2><<<dim3(uint32_t(W / wpb), nmsgs), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire, msgs);
         break;
     default:
-        k_fanout_period<4><<<uint32_t(W / wpb), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire);
+        k_fanout_period<4><<<dim3(uint32_t(W / wpb), nmsgs), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire, msgs);
         break;
     }
     *err = hipGetLastError();
     return true;
+}
+
+// The job's wire offsets on the gather root: every chunk's frame offsets
+// arrive relative to its sender's local wire.
+__global__ __launch_bounds__(BLOCK) void k_rebase_offsets(const uint64_t* __restrict__ stage,
+                                                          const uint64_t* __restrict__ goff, uint64_t n_total,
+                                                          uint32_t chunk, uint64_t* __restrict__ out_off,
+                                                          uint64_t total)
+{
+    const uint64_t stride = uint64_t(gridDim.x) * BLOCK;
+    for (uint64_t g = uint64_t(blockIdx.x) * BLOCK + threadIdx.x; g < n_total; g += stride) {
+        const uint64_t c = g / chunk;
+        out_off[g] = stage[g] - stage[c * chunk] + goff[c];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        out_off[n_total] = total;
+}
+
+hipError_t launch_rebase_offsets(hipStream_t s, const uint64_t* stage, const uint64_t* goff, uint64_t n_total,
+                                 uint32_t chunk, uint64_t* out_off, uint64_t total)
+{
+    const uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>((n_total + BLOCK - 1) / BLOCK, 1), 8192);
+    k_rebase_offsets<<<uint32_t(blocks), BLOCK, 0, s>>>(stage, goff, n_total, chunk, out_off, total);
+    return hipGetLastError();
 }
 
 hipError_t launch_xor(hipStream_t s, int grid, const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,

@@ -21,7 +21,9 @@ def rank_frames(rank, world, n_total, chunk=1024):
 
 
 def gather_frames(wire, wire_off, dst=0, group=None):
-    """Gather every rank's framed output to rank `dst`.
+    """Gather every rank's framed output to rank `dst` with torch.distributed
+    (the gloo path of the CPU tests; the RCCL path of a deployment is the
+    C-ABI's wsg_mgpu_encode_gather, cppserver_amd.MultiGPU).
 
     wire: uint8 tensor (this rank's encoded frames, back to back; at least
     wire_off[-1] bytes); wire_off: int64 tensor of n_local + 1 frame offsets.
@@ -35,11 +37,11 @@ def gather_frames(wire, wire_off, dst=0, group=None):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = wire.device
-    nbytes = int(wire_off[-1].item())
-    sizes = torch.tensor([nbytes, int(wire_off.numel())], dtype=torch.int64, device=dev)
+    sizes = torch.stack([wire_off[-1].to(torch.int64), torch.tensor(wire_off.numel(), device=dev)])
     all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
     dist.all_gather(all_sizes, sizes, group=group)
-    all_sizes = [(int(s[0].item()), int(s[1].item())) for s in all_sizes]
+    all_sizes = torch.stack(all_sizes).cpu().tolist()   # one host sync for every rank's sizes
+    nbytes = all_sizes[rank][0]
 
     if rank != dst:
         ops = [dist.P2POp(dist.isend, wire[:nbytes].contiguous(), dst, group=group),
@@ -68,21 +70,24 @@ def gather_frames(wire, wire_off, dst=0, group=None):
 
 def reassemble(parts, n_total, chunk=1024):
     """Per-rank (wire, wire_off) -> the job's frames in global order (one
-    concatenation of per-chunk slices).  Returns (wire, wire_off)."""
+    concatenation of per-chunk slices).  Returns (wire, wire_off).  The
+    offsets come to the host once per rank (no per-chunk device sync)."""
     import torch
 
     world = len(parts)
     n_chunks = (n_total + chunk - 1) // chunk
-    slices, lens = [], []
+    offs = [off.cpu().numpy() for _, off in parts]
+    slices, sizes = [], []
     for c in range(n_chunks):
         r, j = c % world, c // world
-        w, off = parts[r]
-        lo, hi = j * chunk, min((j + 1) * chunk, int(off.numel()) - 1)
-        a, b = int(off[lo].item()), int(off[hi].item())
-        slices.append(w[a:b])
-        lens.append(off[lo: hi + 1] - off[lo])
-    wire = torch.cat(slices) if slices else torch.empty(0, dtype=torch.uint8)
-    sizes = torch.cat([l[1:] - l[:-1] for l in lens]) if lens else torch.empty(0, dtype=torch.int64)
-    wire_off = torch.zeros(n_total + 1, dtype=torch.int64, device=wire.device)
-    wire_off[1:] = torch.cumsum(sizes, 0)
-    return wire, wire_off
+        w, _ = parts[r]
+        off = offs[r]
+        lo, hi = j * chunk, min((j + 1) * chunk, len(off) - 1)
+        slices.append(w[int(off[lo]): int(off[hi])])
+        sizes.append(np.diff(off[lo: hi + 1]))
+    dev = parts[0][0].device
+    wire = torch.cat(slices) if slices else torch.empty(0, dtype=torch.uint8, device=dev)
+    wire_off = np.zeros(n_total + 1, dtype=np.int64)
+    if sizes:
+        wire_off[1:] = np.cumsum(np.concatenate(sizes))
+    return wire, torch.from_numpy(wire_off).to(dev)

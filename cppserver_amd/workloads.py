@@ -85,6 +85,70 @@ def c5_rank_frames(rank, world, n_total=1 << 20, chunk=1024):
     return rank_frames(rank, world, n_total, chunk)
 
 
+_M32 = 0xFFFFFFFF
+
+
+def _mix32(x, xp):
+    """32-bit integer hash (xorshift-multiply) on non-negative int64/uint64
+    arrays holding 32-bit values; every product stays below 2**63, so numpy
+    (uint64) and torch (int64, CPU or GPU) compute the same words."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x2C1B3C6D) & _M32
+    return x ^ (x >> 12)
+
+
+def c5_key_of(ids):
+    """Key of global frame g (splitmix-like hash of g): the same job at any
+    world size."""
+    g = np.asarray(ids).astype(np.uint64)
+    z = (g + np.uint64(0x9E3779B97F4A7C15)) * np.uint64(0xBF58476D1CE4E5B9)
+    z ^= z >> np.uint64(31)
+    return (z & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
+def c5_payload_np(ids, size=16384):
+    """Payload bytes of global frames `ids` (a function of the frame index
+    only, so any shard of the job regenerates its frames), host numpy."""
+    assert size % 4 == 0
+    w = size // 4
+    g = np.asarray(ids, dtype=np.uint64)[:, None]
+    x = (g * np.uint64(w) + np.arange(w, dtype=np.uint64)[None, :]) & np.uint64(_M32)
+    return _mix32(x, np).astype(np.uint32).view(np.uint8).reshape(-1)
+
+
+def c5_payload_torch(ids, size=16384, device="cuda", step=1 << 14):
+    """c5_payload_np computed on the device (the 16 GiB job of C5 is made in
+    HBM, not on the host): uint8 tensor of len(ids) * size bytes."""
+    import torch
+
+    assert size % 4 == 0
+    w = size // 4
+    ids = torch.as_tensor(np.asarray(ids, dtype=np.int64), device=device)
+    out = torch.empty(len(ids) * size, dtype=torch.uint8, device=device)
+    words = out.view(torch.int32).view(len(ids), w)
+    j = torch.arange(w, dtype=torch.int64, device=device)[None, :]
+    for a in range(0, len(ids), step):
+        g = ids[a: a + step, None]
+        x = (g * w + j) & _M32
+        x = _mix32(x, torch)
+        words[a: a + step] = (x - ((x >> 31) << 32)).to(torch.int32)   # wrap to signed 32-bit
+    return out
+
+
+def c5_desc(ids, size=16384):
+    """Descriptors of a shard whose payloads lie back to back (local order)."""
+    n = len(ids)
+    desc = np.zeros(n, dtype=SEND_DESC)
+    desc["src_off"] = np.arange(n, dtype=np.uint64) * np.uint64(size)
+    desc["len"] = size
+    desc["key"] = c5_key_of(ids)
+    desc["opcode"] = WS_FIN | WS_BINARY
+    desc["mask"] = 1
+    return desc
+
+
 def c5_shard(rank, world, n_total=1 << 20, size=16384, chunk=1024, seed=5, max_frames=None):
     """This rank's encode batch: (payload, desc, frame_ids).  Keys derive from
     the global frame index (shards are disjoint, the key set is the same job

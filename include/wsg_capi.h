@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define WSG_ABI_VERSION 2
+#define WSG_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 #define WSG_OK          0
@@ -122,6 +122,21 @@ int wsg_encode_batch(wsg_ctx* ctx, const uint8_t* d_payload,
 int wsg_fanout_encode(wsg_ctx* ctx, const uint8_t* d_payload, uint64_t len,
                       const uint32_t* d_keys, uint32_t k, uint8_t opcode,
                       int mask, uint8_t* d_wire, uint64_t wire_cap, void* stream);
+
+/* ---- many messages x k keys in one call (a ws_multicast tick) ----------- */
+/* The multicast driver sends `messages_rate` messages per tick to every
+ * client (reference performance/ws_multicast_server.cpp:104-114, each through
+ * WSServer::Multicast, source/server/ws/ws_server.cpp:36-64); this encodes
+ * m messages for k client keys at once.  Frame (i, j) =
+ * PrepareSendFrame(opcode[i], mask, message i, len[i]) with _ws_send_mask =
+ * d_keys[j]; message i's payload is d_payload + src_off[i].  The k frames of
+ * message i lie back to back from wire_off[i] (128-byte aligned; frame j at
+ * wire_off[i] + j * wsg_frame_size(opcode[i], mask, len[i], 0)).
+ * src_off / len / opcode are HOST arrays of m entries; wire_off (host, m + 1
+ * entries) is filled, wire_off[m] = bytes used (checked against wire_cap).   */
+int wsg_fanout_encode_many(wsg_ctx* ctx, const uint8_t* d_payload, const uint64_t* src_off, const uint64_t* len,
+                           const uint8_t* opcode, uint32_t m, const uint32_t* d_keys, uint32_t k, int mask,
+                           uint8_t* d_wire, uint64_t wire_cap, uint64_t* wire_off, void* stream);
 
 /* ---- host-staged entry points (host buffers; PCIe in the path) ---------- */
 /* XOR `len` bytes of host `src` into host `dst` with key byte (phase+i)%4 on
@@ -233,6 +248,42 @@ int wsg_tx_queue(wsg_tx* tx, wsg_session* s, uint8_t opcode, int mask,
 int wsg_tx_forget(wsg_tx* tx, wsg_session* s);
 int wsg_tx_pending(wsg_tx* tx, uint32_t* frames, uint64_t* payload_bytes);
 int wsg_tx_flush(wsg_tx* tx, wsg_tx_sink sink, void* user, uint32_t* sent);
+
+/* ---- multi-GPU: shard, encode, gather to one rank */
+/* BASELINE config C5 (1 Mi x 16 KiB frames on the 8 GPUs of a node): the
+ * reference has no GPU and no collective; a C++ server that owns a node calls
+ * this instead of encoding every frame on its IO threads.  Chunks of `chunk`
+ * consecutive frames are dealt round-robin, chunk c to rank c % world; a
+ * rank's local batch is its chunks in order (wsg_mgpu_shard_count frames).
+ * The gather runs over RCCL (xGMI), loaded at run time.                      */
+typedef struct wsg_mgpu wsg_mgpu;
+#define WSG_MGPU_ID_BYTES 128
+/* One process driving `ndev` GPUs (one ctx and stream per device). */
+int wsg_mgpu_create(const int* devices, int ndev, wsg_mgpu** out);
+/* One rank of a multi-process group (one process per GPU): rank 0 makes the
+ * id with wsg_mgpu_unique_id and the caller hands it to every rank.        */
+int wsg_mgpu_unique_id(uint8_t* id);
+int wsg_mgpu_create_rank(int device, const uint8_t* id, int rank, int world, wsg_mgpu** out);
+int wsg_mgpu_destroy(wsg_mgpu* g);
+/* world size, ranks driven by this process, the first of them */
+int wsg_mgpu_info(wsg_mgpu* g, int* world, int* nlocal, int* first_rank);
+/* codec context of local rank i (its device; wsg_stream gives its stream) */
+wsg_ctx* wsg_mgpu_ctx(wsg_mgpu* g, int i);
+/* frames of an n_total-frame job that `rank` owns */
+uint64_t wsg_mgpu_shard_count(uint64_t n_total, uint32_t chunk, int world, int rank);
+/* Encode every local rank's shard and gather the job's frames, in global
+ * frame order, to rank `root`.  Arrays of nlocal entries, one per local rank
+ * (device buffers on that rank's GPU): d_payload / d_desc / n_local its
+ * shard (as wsg_encode_batch), d_wire / wire_cap / d_wire_off its encoded
+ * shard (n_local + 1 offsets).  On the root: d_out (capacity out_cap) gets
+ * the whole job's wire, d_out_off (n_total + 1, or NULL) its frame offsets.
+ * Synchronous; every rank of the group calls it with the same n_total,
+ * chunk and root.  times (or NULL): {encode ms, gather ms}, max over the
+ * local ranks.                                                              */
+int wsg_mgpu_encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* const* d_payload,
+                           const wsg_send_desc* const* d_desc, const uint32_t* n_local, uint8_t* const* d_wire,
+                           const uint64_t* wire_cap, uint64_t* const* d_wire_off, int root, uint8_t* d_out,
+                           uint64_t out_cap, uint64_t* d_out_off, double* times);
 
 /* ---- kernel timing (measurement hook used by bench.py) ------------------ */
 /* on = k > 0: the ctx records HIP events around the dominant payload kernel of

@@ -43,7 +43,7 @@ def test_library_exports(name):
 
 
 def test_abi_version():
-    assert ca.lib().wsg_abi_version() == 2
+    assert ca.lib().wsg_abi_version() == 3
 
 
 @pytest.mark.parametrize("opcode,mask,length,status", [

@@ -1,0 +1,189 @@
+"""BASELINE config C5 (1 Mi x 16 KiB frames sharded round-robin over the GPUs
+of a node, framed output gathered to one rank) on the GPU.
+
+* the full-size job on one GPU: every one of the 1 Mi frames checked against
+  an independent torch restatement of PrepareSendFrame's bytes
+  (ws.cpp:222-270: header 82 fe 40 00 + key, payload XOR key), and the first
+  64 Ki frames byte for byte against the oracle;
+* the multi-process flow at world size 2 (gloo, both ranks on cuda:0): each
+  rank encodes its shard with the HIP kernels, the shards are gathered and
+  reassembled, and the job equals the oracle's encode of the whole job;
+* the C-ABI multi-GPU entry (wsg_mgpu_encode_gather over RCCL) at world size
+  1 — the only RCCL group one GPU allows — in both of its forms (one process
+  driving its devices; one rank per process), against the oracle.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import cppserver_amd as ca  # noqa: E402
+from cppserver_amd import shard  # noqa: E402
+from cppserver_amd import workloads as wl  # noqa: E402
+from cppserver_amd.layout import SEND_DESC, frame_size  # noqa: E402
+
+SIZE = 16384
+FSZ = frame_size(0x82, True, SIZE)   # 16392: 8-byte header (126 form + key)
+
+
+@pytest.fixture(scope="module")
+def codec():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    c = ca.Codec(0)
+    yield c
+    c.close()
+
+
+def test_c5_payload_generators_agree():
+    ids = np.array([0, 1, 2, 1023, 1024, 77777, (1 << 20) - 1])
+    host = wl.c5_payload_np(ids, SIZE)
+    dev = wl.c5_payload_torch(ids, SIZE, device="cuda").cpu().numpy()
+    assert np.array_equal(host, dev)
+
+
+def _expected_words(ids_dev, keys_dev):
+    """Frame words (int32, little-endian) PrepareSendFrame emits for masked
+    0x82 frames of SIZE bytes: 82 fe 40 00 | key | payload ^ key."""
+    n = ids_dev.numel()
+    pay = wl.c5_payload_torch(ids_dev.cpu().numpy(), SIZE, device="cuda").view(torch.int32).view(n, SIZE // 4)
+    k = keys_dev.view(n, 1)
+    hdr = torch.full((n, 1), 0x0040FE82, dtype=torch.int32, device="cuda")
+    return torch.cat([hdr, k, pay ^ k], dim=1)
+
+
+def test_c5_full_size_one_gpu(codec):
+    n = 1 << 20
+    ids = np.arange(n, dtype=np.int64)
+    payload = wl.c5_payload_torch(ids, SIZE, device="cuda")          # 16 GiB in HBM
+    desc = wl.c5_desc(ids, SIZE)
+    cap = n * FSZ
+    wire, off = codec.encode_batch(payload, ca.desc_to_tensor(desc, "cuda"), wire_cap=cap)
+    codec.sync()
+    offs = off.cpu().numpy()
+    assert np.array_equal(offs, np.arange(n + 1, dtype=np.int64) * FSZ)
+    # every frame against the torch restatement
+    keys = torch.from_numpy(desc["key"].view(np.int32).copy()).cuda()
+    words = wire[:cap].view(torch.int32).view(n, FSZ // 4)
+    step = 1 << 16
+    ids_dev = torch.from_numpy(ids).cuda()
+    for a in range(0, n, step):
+        exp = _expected_words(ids_dev[a: a + step], keys[a: a + step])
+        assert torch.equal(words[a: a + step], exp), "frames %d.." % a
+    # the first 64 Ki frames (1 GiB) byte for byte against the oracle
+    sub = 1 << 16
+    wire_o, off_o = oracle.encode_batch(payload[: sub * SIZE].cpu().numpy(), desc[:sub])
+    assert np.array_equal(wire[: sub * FSZ].cpu().numpy(), wire_o)
+    assert np.array_equal(off_o, offs[: sub + 1].astype(np.uint64))
+    del payload, wire, words
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _gloo_worker(rank, world, port, n_total, chunk, results):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = ca.Codec(0)
+        ids = shard.rank_frames(rank, world, n_total, chunk)
+        payload = wl.c5_payload_torch(ids, SIZE, device="cuda")
+        desc = wl.c5_desc(ids, SIZE)
+        wire, off = c.encode_batch(payload, ca.desc_to_tensor(desc, "cuda"), wire_cap=len(ids) * FSZ)
+        c.sync()
+        parts = shard.gather_frames(wire.cpu(), off.cpu())
+        if rank == 0:
+            got, got_off = shard.reassemble(parts, n_total, chunk)
+            allids = np.arange(n_total)
+            ref, ref_off = oracle.encode_batch(wl.c5_payload_np(allids, SIZE), wl.c5_desc(allids, SIZE))
+            results[0] = bool(np.array_equal(got.numpy(), ref) and
+                              np.array_equal(got_off.numpy().view(np.uint64), ref_off))
+        c.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_total,chunk", [(16384, 1024), (5000, 700)])
+def test_c5_world2_gloo_hip_encode(n_total, chunk):
+    import torch.multiprocessing as mp
+
+    results = mp.Manager().dict()
+    mp.spawn(_gloo_worker, args=(2, _free_port(), n_total, chunk, results), nprocs=2, join=True)
+    assert results.get(0) is True
+
+
+def _ragged_job(n, seed):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 3000, n)
+    big = rng.random(n) < 0.05
+    lens[big] = rng.integers(60000, 70000, int(big.sum()))
+    desc, total = wl.ragged_desc(rng, lens)
+    desc["opcode"] = rng.choice([0x81, 0x82, 0x88, 0x89], n)
+    desc["status"] = np.where(desc["opcode"] == 0x88, 1000, 0)
+    return wl.random_bytes(rng, max(total, 1)), desc
+
+
+def _mgpu_check(g, payload, desc, chunk):
+    n = len(desc)
+    ref, ref_off = oracle.encode_batch(payload, desc)
+    # world 1: the shard is the whole job, in order
+    assert ca.MultiGPU.shard_count(n, chunk, 1, 0) == n
+    cap = int(ref_off[-1]) + 16
+    p = torch.from_numpy(payload).cuda()
+    d = ca.desc_to_tensor(desc, "cuda")
+    wire = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    woff = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    out = torch.full((cap + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    out_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    enc_ms, gat_ms = g.encode_gather(n, chunk, [p], [d], [wire], [woff], root=0, out=out, out_off=out_off)
+    got = out.cpu().numpy()
+    assert np.array_equal(got[: len(ref)], ref)
+    assert (got[len(ref):] == 0xA5).all()
+    assert np.array_equal(out_off.cpu().numpy().view(np.uint64), ref_off)
+    assert enc_ms >= 0 and gat_ms >= 0
+
+
+@pytest.mark.parametrize("n,chunk", [(3000, 1024), (1000, 1), (4096, 1024)])
+def test_mgpu_single_process_world1(n, chunk):
+    g = ca.MultiGPU([0])
+    assert (g.world, g.nlocal, g.first_rank) == (1, 1, 0)
+    try:
+        _mgpu_check(g, *_ragged_job(n, seed=n + chunk), chunk)
+    finally:
+        g.close()
+
+
+def test_mgpu_rank_world1_c5_shape():
+    g = ca.MultiGPU.rank(0, ca.MultiGPU.unique_id(), 0, 1)
+    try:
+        ids = np.arange(4096)
+        _mgpu_check(g, wl.c5_payload_np(ids, SIZE), wl.c5_desc(ids, SIZE), 1024)
+    finally:
+        g.close()
+
+
+def test_mgpu_rejects_wrong_shard():
+    g = ca.MultiGPU([0])
+    try:
+        payload, desc = _ragged_job(100, seed=3)
+        p = torch.from_numpy(payload).cuda()
+        d = ca.desc_to_tensor(desc[:50], "cuda")   # half the job is not world 1's shard
+        w = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
+        o = torch.empty(51, dtype=torch.int64, device="cuda")
+        with pytest.raises(ca.WSGError) as e:
+            g.encode_gather(100, 10, [p], [d], [w], [o], out=w.clone())
+        assert e.value.code == ca.WSG_EINVAL
+    finally:
+        g.close()

@@ -413,6 +413,53 @@ def test_fanout_period_path(codec, length, k, opcode, mask, src_off):
     assert (got[len(ref):] == 0xA5).all()
 
 
+@pytest.mark.parametrize("case", ["c4x16", "mixed", "many-groups", "flat-sizes"])
+def test_fanout_many_vs_oracle(codec, case):
+    """wsg_fanout_encode_many: m messages x k keys in one call (one launch per
+    group of up to 32 same-geometry messages), each message's frames equal to
+    oracle.fanout_encode of that message; nothing written outside them."""
+    rng = np.random.default_rng(sum(map(ord, case)))
+    if case == "c4x16":        # the multicast tick at C4's shape
+        m, k = 16, 10000
+        lens = np.full(m, 4096)
+        ops = np.full(m, 0x82)
+    elif case == "mixed":      # lengths / opcodes differ: several launches, status-prefixed ping (Q2)
+        m, k = 9, 300
+        lens = np.array([4096, 4096, 100, 4096, 1016, 65538, 4096, 0, 2040])
+        ops = np.array([0x82, 0x81, 0x82, 0x82, 0x89, 0x82, 0x82, 0x88, 0x8A])
+    elif case == "many-groups":  # more than 32 messages of one geometry: two launches
+        m, k = 70, 257
+        lens = np.full(m, 4088)
+        ops = np.full(m, 0x82)
+    else:                      # frame sizes the period path does not take (flat kernel per message)
+        m, k = 5, 123
+        lens = np.array([4097, 1, 30, 12290, 4097])
+        ops = np.array([0x82, 0x81, 0x82, 0x82, 0x82])
+    keys = rng.integers(0, 2**32, k, dtype=np.uint64).astype(np.uint32)
+    src = np.zeros(m, np.uint64)
+    src[1:] = np.cumsum(lens[:-1] + 3)           # unaligned message starts
+    arena = wl.random_bytes(rng, int(src[-1] + lens[-1] + 16))
+    for mask in (True, False):
+        wire_t, off = codec.fanout_many(dev(arena), src, lens, ops, dev(keys.view(np.int32)), mask=mask)
+        codec.sync()
+        got = wire_t.cpu().numpy()
+        for i in range(m):
+            msg = arena[int(src[i]): int(src[i]) + int(lens[i])]
+            ref = oracle.fanout_encode(msg, keys, int(ops[i]), mask)
+            a = int(off[i])
+            assert a % 128 == 0
+            assert np.array_equal(got[a: a + len(ref)], ref), (i, mask)
+        assert int(off[m]) == int(off[m - 1]) + k * frame_size(int(ops[-1]), mask, int(lens[-1]))
+
+
+def test_fanout_many_capacity(codec):
+    keys = torch.zeros(4, dtype=torch.int32, device="cuda")
+    with pytest.raises(ca.WSGError) as e:
+        codec.fanout_many(torch.zeros(64, dtype=torch.uint8, device="cuda"), [0, 0], [10, 10], [0x82, 0x82], keys,
+                          wire=torch.zeros(64, dtype=torch.uint8, device="cuda"))
+    assert e.value.code == ca.WSG_ENOMEM
+
+
 # ---------------------------------------------------------------- edge cases
 def test_empty_batches(codec):
     rc, out, info = gpu_decode(codec, np.zeros(32, np.uint8), [])

@@ -282,6 +282,43 @@ __global__ __launch_bounds__(256) void k_pipe(const u32x4* __restrict__ src, u32
     }
 }
 
+// Cache-policy variants of the 16 KiB-tile copy (decode's shape): buffer
+// loads/stores with the gfx950 cache-policy bits in `aux` (1 = sc0, 2 = nt,
+// 16 = sc1); LA / SA = load / store policy; LA = 255 reads nothing (write-only),
+// SA = 255 stores nothing (read-only, XOR-reduced).
+template <int LA, int SA>
+__global__ __launch_bounds__(256) void k_policy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                uint64_t tiles, uint32_t key)
+{
+    constexpr uint64_t TB = 16384;
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        u32x4 v[4];
+        if (LA != 255) {
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src) + t * TB, 0, TB, 0x00020000);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * 256 + threadIdx.x) * 16, 0, LA);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                v[u] = u32x4{uint32_t(t), uint32_t(u), threadIdx.x, key};
+        }
+        if (SA != 255) {
+            const auto rd = __builtin_amdgcn_make_buffer_rsrc(dst + t * TB, 0, TB, 0x00020000);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                __builtin_amdgcn_raw_buffer_store_b128(v[u] ^ key, rd, (u * 256 + threadIdx.x) * 16, 0, SA);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                acc ^= v[u];
+        }
+    }
+    if (SA == 255 && acc.x == 0xdeadbeefu && acc.y == 0x01234567u)
+        reinterpret_cast<u32x4*>(dst)[threadIdx.x] = acc;
+}
+
 template <class F>
 double time_kernel(F launch, int reps = 20)
 {
@@ -376,6 +413,37 @@ int main(int argc, char** argv)
     printf("device %s CUs=%d bytes=%llu MiB\n", p.gcnArchName, cus, (unsigned long long)mib);
     if (argc > 2 && std::string(argv[2]) == "explore")
         return explore(bytes, cus);
+    if (argc > 2 && std::string(argv[2]) == "policy") {
+        // cache-policy bits on loads/stores of the decode-shaped copy at the
+        // C2 footprint (argv[1] MiB), two buffer pairs in turn, 48 blocks/CU;
+        // then in place, then write-only / read-only per policy
+        const uint64_t span = 4 * bytes;
+        uint8_t* base;
+        CK(hipMalloc(&base, span));
+        CK(hipMemset(base, 5, span));
+        const uint64_t tiles = bytes / 16384;
+        auto gbs = [&](double ms, double mult) { return mult * bytes / (ms * 1e-3) / 1e9; };
+#define POL(LA, SA, INPLACE, MULT)                                                                             \
+    for (int bpc : {32, 48}) {                                                                                 \
+        const int grid = int(std::min<uint64_t>(tiles, uint64_t(cus) * bpc));                                 \
+        double ms = time_kernel([&](int i) {                                                                   \
+            const uint64_t s = (i & 1) * 2 * bytes;                                                            \
+            k_policy<LA, SA><<<grid, 256>>>(base + s, base + s + (INPLACE ? 0 : bytes), tiles, 9u);           \
+        });                                                                                                    \
+        printf("policy load=%3d store=%3d inplace=%d bpc=%2d %8.1f us %7.1f GB/s\n", LA, SA, INPLACE, bpc,      \
+               ms * 1e3, gbs(ms, MULT));                                                                       \
+    }
+        for (int rep = 0; rep < 2; ++rep) {
+            POL(2, 2, 0, 2) POL(0, 0, 0, 2) POL(2, 0, 0, 2) POL(2, 16, 0, 2) POL(2, 17, 0, 2) POL(2, 18, 0, 2)
+            POL(2, 3, 0, 2) POL(2, 1, 0, 2) POL(16, 2, 0, 2) POL(18, 2, 0, 2) POL(3, 2, 0, 2)
+            POL(2, 2, 1, 2) POL(2, 16, 1, 2) POL(2, 18, 1, 2)
+            POL(255, 2, 0, 1) POL(255, 0, 0, 1) POL(255, 16, 0, 1) POL(255, 17, 0, 1) POL(255, 18, 0, 1)
+            POL(2, 255, 0, 1) POL(0, 255, 0, 1) POL(16, 255, 0, 1) POL(18, 255, 0, 1)
+        }
+#undef POL
+        CK(hipFree(base));
+        return 0;
+    }
     if (argc > 2 && std::string(argv[2]) == "grid") {
         // copy ceiling against the grid: 16 KiB block tiles and 4 KiB wave
         // pieces, from grid-stride (8 blocks/CU) to one unit per block/wave;
