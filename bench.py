@@ -489,6 +489,36 @@ def session_batch_leg(timeout=240):
     return out
 
 
+def echo_c1_leg(seconds=3.0, timeout=120):
+    """BASELINE config C1 (ws_echo_client / ws_echo_server: 32-byte messages,
+    1000 in flight per client) through the drop-in WSClient / WSSession API
+    over in-memory transports (tools/_build/bench_echo, product library only;
+    no sockets: the transport is out of scope).  per_read = the API's default
+    (each read one batch scope), tick = one scope per event-loop pass,
+    per_call = automatic batching off (one GPU round trip per masked frame).
+    Metric as ws_echo_client.cpp:191-201 (messages = echoed bytes / size)."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "tools", "_build", "bench_echo")
+    if not os.path.exists(exe):
+        return None
+    out = {}
+    legs = (("per_read_1c", ["per_read", "1", "1", "1000", "32"]),
+            ("per_read_100c_4t", ["per_read", "100", "4", "1000", "32"]),
+            ("tick_100c_1t", ["tick", "100", "1", "1000", "32"]),
+            ("per_call_1c", ["per_call", "1", "1", "1000", "32"]))
+    for leg, args in legs:
+        r = subprocess.run([exe] + args + [str(seconds)], capture_output=True, text=True, timeout=timeout)
+        if r.returncode != 0:
+            out[leg] = {"error": (r.stderr or r.stdout).strip()[-300:]}
+            continue
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        out[leg] = {k: d[k] for k in ("msg_per_s", "MiB_per_s", "latency_ns", "total_messages", "payload_ok")}
+    out["reference_published"] = {"msg_per_s_1c_1t": 160448, "msg_per_s_100c_4t": 594328,
+                                  "hardware": "i7-4790K, loopback sockets (README.md:3312-3352)"}
+    return out
+
+
 def echo_size_leg(w, n=1 << 20, size=32, reps=20):
     """Echo-sized frames on the device batch paths (SURVEY C1's 32 B messages,
     38 B masked client frames): one batch of 1 Mi frames encoded
@@ -782,6 +812,9 @@ def main():
             sb = session_batch_leg()
             if sb is not None:
                 extras["session_batch"] = sb
+            c1 = echo_c1_leg()
+            if c1 is not None:
+                extras["echo_c1"] = c1
     cpu1 = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu1, cpu_mt = cpu_baseline(w, args.cpu_seconds, host_cpu())

@@ -102,6 +102,8 @@ def lib(path=None):
         "wsg_timing_read": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ci]),
     }
     for name, (res, args) in sig.items():
+        if path is not None and not hasattr(L, name):
+            continue   # an older A/B build of the library (tools/): bind what it has
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -226,6 +228,9 @@ class Codec:
         if wire is None:
             wire = t.empty(max(int(wire_cap), 16), dtype=t.uint8, device=desc.device)
         cap = int(wire.numel()) if wire_cap is None else int(wire_cap)
+        if cap > int(wire.numel()):
+            raise WSGError(WSG_EINVAL, "encode_batch: wire_cap %d exceeds the wire tensor (%d bytes)"
+                           % (cap, int(wire.numel())))
         if wire_off is None:
             wire_off = t.empty(n + 1, dtype=t.int64, device=desc.device)
         rc = self._L.wsg_encode_batch(self._ctx, ctypes.c_void_p(payload.data_ptr()),

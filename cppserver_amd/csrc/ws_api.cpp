@@ -50,8 +50,17 @@ void WSClient::ResetBuffers()
 {
     if (_rx_batch)
         _rx_batch->Clear(*this);   // message state resets in delivery order
+    else if (BatchScope::Active())
+        BatchScope::Receive().Clear(*this);
     else
         ClearWSBuffers();
+}
+
+WSClient::~WSClient()
+{
+    // frames still queued on this thread's automatic batches
+    BatchScope::Receive().Forget(*this);
+    BatchScope::Send().Forget(_transport);
 }
 
 void WSClient::SetReceiveBatch(WSReceiveBatch* batch)
@@ -93,6 +102,9 @@ void WSClient::onDisconnected()
 
 void WSClient::onReceived(const void* buffer, size_t size)
 {
+    // everything this read triggers (onWS* callbacks, their Send*Async) is
+    // batched on this thread and flushed when the outermost scope closes
+    BatchScope scope;
     if (!_ws_handshaked) {
         // the upgrade response (reference ws_client.cpp:76-116 via HTTPClient)
         _http_buf.append(static_cast<const char*>(buffer), size);
@@ -108,18 +120,22 @@ void WSClient::onReceived(const void* buffer, size_t size)
         }
         if (!PerformClientUpgrade(response) || rest.empty())
             return;
-        buffer = rest.data();   // frames that came with the response
-        size = rest.size();
-        if (_rx_batch)
-            _rx_batch->Feed(*this, buffer, size);
-        else
-            PrepareReceiveFrame(buffer, size);
+        RouteFrames(rest.data(), rest.size());   // frames that came with the response
         return;
     }
-    if (_rx_batch)
+    RouteFrames(buffer, size);
+}
+
+void WSClient::RouteFrames(const void* buffer, size_t size)
+{
+    if (_rx_batch) {
         _rx_batch->Feed(*this, buffer, size);
-    else
+    } else if (BatchScope::Active()) {
+        BatchScope::Receive().Feed(*this, buffer, size);
+        BatchScope::CheckLimits();
+    } else {
         PrepareReceiveFrame(buffer, size);
+    }
 }
 
 void WSClient::SetSendBatch(WSSendBatch* batch)
@@ -134,6 +150,8 @@ size_t WSClient::SendFrame(uint8_t opcode, const void* buffer, size_t size, int 
 {
     if (_tx_batch)
         _tx_batch->Flush();   // earlier async frames go first
+    else if (BatchScope::Active())
+        BatchScope::Send().Flush();
     std::scoped_lock locker(_ws_send_lock);
     PrepareSendFrame(opcode, true, buffer, size, status);
     return _transport.Send(_ws_send_buffer.data(), _ws_send_buffer.size());
@@ -141,19 +159,28 @@ size_t WSClient::SendFrame(uint8_t opcode, const void* buffer, size_t size, int 
 
 bool WSClient::SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status)
 {
-    std::scoped_lock locker(_ws_send_lock);
-    if (_tx_batch) {
-        _tx_batch->Queue(_transport, send_key(), opcode, true, buffer, size, status);
-        return true;
+    {
+        std::scoped_lock locker(_ws_send_lock);
+        if (_tx_batch) {
+            _tx_batch->Queue(_transport, send_key(), opcode, true, buffer, size, status);
+            return true;
+        }
+        if (!BatchScope::Active()) {
+            PrepareSendFrame(opcode, true, buffer, size, status);
+            return _transport.SendAsync(_ws_send_buffer.data(), _ws_send_buffer.size());
+        }
+        BatchScope::Send().Queue(_transport, send_key(), opcode, true, buffer, size, status);
     }
-    PrepareSendFrame(opcode, true, buffer, size, status);
-    return _transport.SendAsync(_ws_send_buffer.data(), _ws_send_buffer.size());
+    BatchScope::CheckLimits();   // not under the send lock: a flush may fire callbacks
+    return true;
 }
 
 bool WSClient::ReceiveMessage(std::vector<uint8_t>& out)
 {
     if (!_ws_handshaked)
         return false;
+    if (BatchScope::Active())
+        BatchScope::Send().Flush();   // what this thread queued goes out before it waits
     return receive_message(
         out, [this]() { return RequiredReceiveFrameSize(); },
         [this](const void* b, size_t n) { PrepareReceiveFrame(b, n); },
@@ -182,8 +209,16 @@ void WSSession::ResetBuffers()
 {
     if (_rx_batch)
         _rx_batch->Clear(*this);   // message state resets in delivery order
+    else if (BatchScope::Active())
+        BatchScope::Receive().Clear(*this);
     else
         ClearWSBuffers();
+}
+
+WSSession::~WSSession()
+{
+    BatchScope::Receive().Forget(*this);
+    BatchScope::Send().Forget(_transport);
 }
 
 void WSSession::SetReceiveBatch(WSReceiveBatch* batch)
@@ -221,6 +256,7 @@ void WSSession::onDisconnected()
 
 void WSSession::onReceived(const void* buffer, size_t size)
 {
+    BatchScope scope;   // as WSClient::onReceived
     if (!_ws_handshaked) {
         // the upgrade request (reference ws_session.cpp:53-65 via HTTPSession)
         _http_buf.append(static_cast<const char*>(buffer), size);
@@ -238,16 +274,22 @@ void WSSession::onReceived(const void* buffer, size_t size)
         }
         if (!PerformServerUpgrade(request, response) || rest.empty())
             return;
-        if (_rx_batch)
-            _rx_batch->Feed(*this, rest.data(), rest.size());
-        else
-            PrepareReceiveFrame(rest.data(), rest.size());
+        RouteFrames(rest.data(), rest.size());
         return;
     }
-    if (_rx_batch)
+    RouteFrames(buffer, size);
+}
+
+void WSSession::RouteFrames(const void* buffer, size_t size)
+{
+    if (_rx_batch) {
         _rx_batch->Feed(*this, buffer, size);
-    else
+    } else if (BatchScope::Active()) {
+        BatchScope::Receive().Feed(*this, buffer, size);
+        BatchScope::CheckLimits();
+    } else {
         PrepareReceiveFrame(buffer, size);
+    }
 }
 
 void WSSession::SetSendBatch(WSSendBatch* batch)
@@ -262,6 +304,8 @@ size_t WSSession::SendFrame(uint8_t opcode, const void* buffer, size_t size, int
 {
     if (_tx_batch)
         _tx_batch->Flush();   // earlier async frames go first
+    else if (BatchScope::Active())
+        BatchScope::Send().Flush();
     std::scoped_lock locker(_ws_send_lock);
     PrepareSendFrame(opcode, false, buffer, size, status);
     return _transport.Send(_ws_send_buffer.data(), _ws_send_buffer.size());
@@ -269,19 +313,28 @@ size_t WSSession::SendFrame(uint8_t opcode, const void* buffer, size_t size, int
 
 bool WSSession::SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status)
 {
-    std::scoped_lock locker(_ws_send_lock);
-    if (_tx_batch) {
-        _tx_batch->Queue(_transport, send_key(), opcode, false, buffer, size, status);
-        return true;
+    {
+        std::scoped_lock locker(_ws_send_lock);
+        if (_tx_batch) {
+            _tx_batch->Queue(_transport, send_key(), opcode, false, buffer, size, status);
+            return true;
+        }
+        if (!BatchScope::Active()) {
+            PrepareSendFrame(opcode, false, buffer, size, status);
+            return _transport.SendAsync(_ws_send_buffer.data(), _ws_send_buffer.size());
+        }
+        BatchScope::Send().Queue(_transport, send_key(), opcode, false, buffer, size, status);
     }
-    PrepareSendFrame(opcode, false, buffer, size, status);
-    return _transport.SendAsync(_ws_send_buffer.data(), _ws_send_buffer.size());
+    BatchScope::CheckLimits();
+    return true;
 }
 
 bool WSSession::ReceiveMessage(std::vector<uint8_t>& out)
 {
     if (!_ws_handshaked)
         return false;
+    if (BatchScope::Active())
+        BatchScope::Send().Flush();
     return receive_message(
         out, [this]() { return RequiredReceiveFrameSize(); },
         [this](const void* b, size_t n) { PrepareReceiveFrame(b, n); },
@@ -310,6 +363,7 @@ void WSServer::AddSession(const std::shared_ptr<WSSession>& session)
 {
     std::unique_lock<std::shared_mutex> locker(_sessions_lock);
     _sessions.push_back(session);
+    _snapshot = std::make_shared<const std::vector<std::shared_ptr<WSSession>>>(_sessions);
     if (_rx_batch)
         session->SetReceiveBatch(_rx_batch.get());
     if (_tx_batch)
@@ -326,6 +380,7 @@ void WSServer::RemoveSession(const std::shared_ptr<WSSession>& session)
             session->SetSendBatch(nullptr);
     }
     _sessions.erase(std::remove(_sessions.begin(), _sessions.end(), session), _sessions.end());
+    _snapshot = std::make_shared<const std::vector<std::shared_ptr<WSSession>>>(_sessions);
 }
 
 void WSServer::EnableBatchReceive(bool on)
@@ -334,7 +389,7 @@ void WSServer::EnableBatchReceive(bool on)
     if (on == (_rx_batch != nullptr))
         return;
     if (on) {
-        _rx_batch = std::make_unique<WSReceiveBatch>(codec());
+        _rx_batch = std::make_unique<WSReceiveBatch>(nullptr);   // flushes decode on the flushing thread's codec
         for (auto& s : _sessions)
             s->SetReceiveBatch(_rx_batch.get());
         return;
@@ -352,7 +407,7 @@ void WSServer::EnableBatchSend(bool on)
     if (on == (_tx_batch != nullptr))
         return;
     if (on) {
-        _tx_batch = std::make_unique<WSSendBatch>(codec());
+        _tx_batch = std::make_unique<WSSendBatch>(nullptr);
         for (auto& s : _sessions)
             s->SetSendBatch(_tx_batch.get());
         return;
@@ -384,6 +439,8 @@ bool WSServer::Multicast(const void* buffer, size_t size)
         return false;
     if (_tx_batch)
         _tx_batch->Flush();   // queued frames precede the multicast on every session
+    else if (BatchScope::Active())
+        BatchScope::Send().Flush();
     std::shared_lock<std::shared_mutex> locker(_sessions_lock);
     for (auto& session : _sessions) {
         std::scoped_lock ws_locker(session->_ws_send_lock);
@@ -395,6 +452,37 @@ bool WSServer::Multicast(const void* buffer, size_t size)
 
 size_t WSServer::MulticastFrame(uint8_t opcode, const void* buffer, size_t size)
 {
+    WSSendBatch* batch = _tx_batch ? _tx_batch.get() : BatchScope::Active() ? &BatchScope::Send() : nullptr;
+    if (batch && size) {
+        // batched: the frame is encoded with the batch's other frames (one
+        // GPU pass per tick, ws_multicast's `messages_rate` calls included)
+        // and then queued on every session that was registered at this call
+        // and is handshaked at the flush
+        std::shared_ptr<const std::vector<std::shared_ptr<WSSession>>> group;
+        {
+            std::shared_lock<std::shared_mutex> locker(_sessions_lock);
+            group = _snapshot;
+        }
+        uint32_t key;
+        {
+            std::scoped_lock locker(_ws_send_lock);
+            key = send_key();
+        }
+        batch->QueueFanout(
+            [group](const uint8_t* frame, size_t len) {
+                if (!group)
+                    return;
+                for (const auto& session : *group) {
+                    std::scoped_lock ws_locker(session->_ws_send_lock);
+                    if (session->_ws_handshaked)
+                        session->_transport.SendAsync(frame, len);
+                }
+            },
+            key, opcode, false, buffer, size);
+        if (batch != _tx_batch.get())
+            BatchScope::CheckLimits();
+        return true;   // the reference returns Multicast()'s bool (ws_server.h:50-59)
+    }
     std::scoped_lock locker(_ws_send_lock);
     PrepareSendFrame(opcode, false, buffer, size);
     return Multicast(_ws_send_buffer.data(), _ws_send_buffer.size());

@@ -11,6 +11,7 @@
 #include "ws_session_impl.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <stdexcept>
@@ -73,6 +74,9 @@ void WSReceiveBatch::Emit(WebSocket& ws, const uint8_t* frame, uint64_t total, u
     // kernel reads the key from the frame, so give it the reference's key.
     if (key)
         std::memcpy(dst + hdr - 4, key, 4);
+    // masked frames (MASK bit) with a nonzero key need the unmask pass
+    if ((frame[1] & 0x80) && (dst[hdr - 4] | dst[hdr - 3] | dst[hdr - 2] | dst[hdr - 1]))
+        b.keyed = true;
     b.recs.push_back(Rec{&ws, int64_t(b.fs.size()), ws._ws_opcode, (frame[0] & 0x80) != 0});
     b.fs.push_back(b.wire.len);
     b.wire.len += total;
@@ -80,6 +84,7 @@ void WSReceiveBatch::Emit(WebSocket& ws, const uint8_t* frame, uint64_t total, u
 
 void WSReceiveBatch::Feed(WebSocket& ws, const void* buffer, size_t size)
 {
+    std::scoped_lock locker(_lock);
     const uint8_t* data = static_cast<const uint8_t*>(buffer);
     auto& fb = ws._ws_receive_frame_buffer;
     do {
@@ -154,12 +159,14 @@ void WSReceiveBatch::Feed(WebSocket& ws, const void* buffer, size_t size)
 
 void WSReceiveBatch::Clear(WebSocket& ws)
 {
+    std::scoped_lock locker(_lock);
     ws.ClearWSBuffers();
     _cur.recs.push_back(Rec{&ws, -1, 0, false});
 }
 
 void WSReceiveBatch::Forget(WebSocket& ws)
 {
+    std::scoped_lock locker(_lock);
     for (Batch* b : {&_cur, &_spare})
         for (Rec& r : b->recs)
             if (r.ws == &ws)
@@ -168,34 +175,58 @@ void WSReceiveBatch::Forget(WebSocket& ws)
 
 size_t WSReceiveBatch::Flush()
 {
-    if (_flushing || _cur.recs.empty())
-        return 0;
-    std::swap(_cur, _spare);
-    _cur.reset();
-    Batch& b = _spare;
-    _flushing = true;
+    {
+        std::scoped_lock locker(_lock);
+        if (_flushing || _cur.recs.empty())
+            return 0;
+        std::swap(_cur, _spare);
+        _cur.reset();
+        _flushing = true;
+    }
+    Batch& b = _spare;   // this thread's until _flushing drops: Feed only touches _cur
     struct Done {
         WSReceiveBatch* t;
         ~Done()
         {
+            std::scoped_lock locker(t->_lock);
             t->_flushing = false;
             t->_spare.reset();
         }
     } done{this};
 
     const size_t n = b.fs.size();
+    const uint8_t* payload_base = b.out.p;
     if (n) {
         if (n > UINT32_MAX)
             throw std::length_error("WSReceiveBatch: more than 2^32-1 frames in one flush");
-        Grow(b.out, b.wire.len);
         b.info.resize(n);
-        check(wsg_decode_batch_host(_ctx ? _ctx : ThreadCodec(), b.wire.p, b.wire.len, b.fs.data(), uint32_t(n),
-                                    b.out.p, b.info.data()),
-              "wsg_decode_batch_host");
+        if (b.keyed) {
+            Grow(b.out, b.wire.len);
+            payload_base = b.out.p;
+            check(wsg_decode_batch_host(_ctx ? _ctx : ThreadCodec(), b.wire.p, b.wire.len, b.fs.data(),
+                                        uint32_t(n), b.out.p, b.info.data()),
+                  "wsg_decode_batch_host");
+        } else {
+            // no frame has a key to apply (unmasked frames, or key 0: the
+            // server-to-client direction of every reference session,
+            // ws.cpp:206): unmasking is the identity, exactly as the
+            // per-call path skips it, so the payloads are handed out where
+            // they lie in the batch; only the headers are read
+            payload_base = b.wire.p;
+            for (size_t i = 0; i < n; ++i) {
+                const uint64_t end = i + 1 < n ? b.fs[i + 1] : b.wire.len;
+                check(wsg_header_unpack(b.wire.p + b.fs[i], end - b.fs[i], &b.info[i]), "wsg_header_unpack");
+                b.info[i].payload_off += b.fs[i];
+            }
+        }
     }
     size_t delivered = 0;
     for (size_t r = 0; r < b.recs.size(); ++r) {
-        const Rec rec = b.recs[r];   // a callback may Forget() a connection: re-read each record
+        Rec rec;
+        {
+            std::scoped_lock locker(_lock);   // a callback / another thread may Forget() a connection
+            rec = b.recs[r];
+        }
         if (!rec.ws)
             continue;
         if (rec.frame < 0) {
@@ -205,7 +236,7 @@ size_t WSReceiveBatch::Flush()
         const wsg_recv_info& in = b.info[size_t(rec.frame)];
         if (in.error)
             throw std::runtime_error("WSReceiveBatch: decode rejected a framed frame");
-        rec.ws->DeliverFrame(rec.opcode, rec.fin, b.out.p + in.payload_off, size_t(in.len));
+        rec.ws->DeliverFrame(rec.opcode, rec.fin, payload_base + in.payload_off, size_t(in.len));
         ++delivered;
     }
     return delivered;
@@ -236,98 +267,269 @@ WSSendBatch::WSSendBatch(wsg_ctx* codec) : _ctx(codec) {}
 
 WSSendBatch::~WSSendBatch()
 {
-    if (_payload.p)
-        wsg_host_free(_payload.p);
-    if (_wire.p)
-        wsg_host_free(_wire.p);
+    for (Pinned* p : {&_q.payload, &_inflight.payload, &_wire})
+        if (p->p)
+            wsg_host_free(p->p);
 }
 
-void WSSendBatch::Push(Transport* t, void* tag, uint32_t key, uint8_t opcode, bool mask, const void* buffer,
-                       size_t size, int status)
+void WSSendBatch::Push(Rec rec, uint32_t key, uint8_t opcode, bool mask, const void* buffer, size_t size,
+                       int status)
 {
     if (size && !buffer)
         throw std::invalid_argument("WSSendBatch: null payload");
-    grow_pinned(_payload.p, _payload.cap, _payload.len, _payload.len + size);
+    std::scoped_lock locker(_lock);
+    Pinned& pl = _q.payload;
+    grow_pinned(pl.p, pl.cap, pl.len, pl.len + size);
     wsg_send_desc d{};
-    d.src_off = _payload.len;
+    d.src_off = pl.len;
     d.len = size;
     d.key = key;
     d.status = status;
     d.opcode = opcode;
     d.mask = mask ? 1 : 0;
     if (size)
-        std::memcpy(_payload.p + _payload.len, buffer, size);
-    _payload.len += size;
-    _desc.push_back(d);
-    _recs.push_back(Rec{t, tag});
+        std::memcpy(pl.p + pl.len, buffer, size);
+    pl.len += size;
+    _q.desc.push_back(d);
+    _q.recs.push_back(std::move(rec));
 }
 
 void WSSendBatch::Queue(Transport& transport, uint32_t key, uint8_t opcode, bool mask, const void* buffer,
                         size_t size, int status)
 {
-    Push(&transport, nullptr, key, opcode, mask, buffer, size, status);
+    Push(Rec{&transport, nullptr, nullptr}, key, opcode, mask, buffer, size, status);
 }
 
 void WSSendBatch::Queue(void* tag, uint32_t key, uint8_t opcode, bool mask, const void* buffer, size_t size,
                         int status)
 {
-    Push(nullptr, tag, key, opcode, mask, buffer, size, status);
+    Push(Rec{nullptr, tag, nullptr}, key, opcode, mask, buffer, size, status);
+}
+
+void WSSendBatch::QueueFanout(std::function<void(const uint8_t*, size_t)> deliver, uint32_t key, uint8_t opcode,
+                              bool mask, const void* buffer, size_t size, int status)
+{
+    Push(Rec{nullptr, nullptr, std::make_shared<std::function<void(const uint8_t*, size_t)>>(std::move(deliver))},
+         key, opcode, mask, buffer, size, status);
 }
 
 void WSSendBatch::Forget(Transport& transport)
 {
-    for (Rec& r : _recs)
-        if (r.transport == &transport)
-            r = Rec{nullptr, nullptr};
+    std::scoped_lock locker(_lock);
+    for (Queue_* q : {&_q, &_inflight})
+        for (Rec& r : q->recs)
+            if (r.transport == &transport)
+                r = Rec{nullptr, nullptr, nullptr};
 }
 
 void WSSendBatch::Forget(void* tag)
 {
-    for (Rec& r : _recs)
-        if (r.tag == tag && !r.transport)
-            r = Rec{nullptr, nullptr};
+    std::scoped_lock locker(_lock);
+    for (Queue_* q : {&_q, &_inflight})
+        for (Rec& r : q->recs)
+            if (r.tag == tag && !r.transport)
+                r = Rec{nullptr, nullptr, nullptr};
 }
 
 size_t WSSendBatch::Flush(Sink sink, void* user)
 {
-    if (_flushing || _desc.empty())
-        return 0;
-    if (_desc.size() > UINT32_MAX)
-        throw std::length_error("WSSendBatch: more than 2^32-1 frames in one flush");
-    _flushing = true;
+    {
+        std::scoped_lock locker(_lock);
+        if (_flushing || _q.desc.empty())
+            return 0;
+        std::swap(_q, _inflight);   // the queue is empty again: callers may queue while this encodes
+        _q.payload.len = 0;
+        _q.desc.clear();
+        _q.recs.clear();
+        _flushing = true;
+    }
     struct Done {
         WSSendBatch* t;
-        ~Done() { t->_flushing = false; }
+        ~Done()
+        {
+            std::scoped_lock locker(t->_lock);
+            t->_flushing = false;
+            t->_inflight.payload.len = 0;
+            t->_inflight.desc.clear();
+            t->_inflight.recs.clear();
+        }
     } done{this};
-    const uint32_t n = uint32_t(_desc.size());
+    Queue_& b = _inflight;
+    if (b.desc.size() > UINT32_MAX)
+        throw std::length_error("WSSendBatch: more than 2^32-1 frames in one flush");
+    const uint32_t n = uint32_t(b.desc.size());
     uint64_t total = 0;
-    for (const wsg_send_desc& d : _desc)
+    for (const wsg_send_desc& d : b.desc)
         total += wsg_frame_size(d.opcode, d.mask, d.len, d.status);
     grow_pinned(_wire.p, _wire.cap, 0, std::max<uint64_t>(total, 1));
     _wire_off.resize(size_t(n) + 1);
-    check(wsg_encode_batch_host(_ctx ? _ctx : ThreadCodec(), _payload.p, _payload.len, _desc.data(), n, _wire.p,
-                                _wire.cap, _wire_off.data()),
-          "wsg_encode_batch_host");
-    // encoded: the queue is empty again before any frame is handed out, so a
-    // transport's SendAsync may queue more frames (they go with the next
-    // flush); if the encode failed above, everything stays queued
-    std::vector<Rec> recs;
-    recs.swap(_recs);
-    _desc.clear();
-    _payload.len = 0;
+    bool keyed = false;
+    for (const wsg_send_desc& d : b.desc)
+        keyed = keyed || d.key != 0;
+    int rc = WSG_OK;
+    if (keyed) {
+        rc = wsg_encode_batch_host(_ctx ? _ctx : ThreadCodec(), b.payload.p, b.payload.len, b.desc.data(), n,
+                                   _wire.p, _wire.cap, _wire_off.data());
+    } else {
+        // every frame has key 0 (server sessions, ws.cpp:206): the XOR is the
+        // identity, as on the per-call path; header + status + payload copy
+        uint64_t at = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            const wsg_send_desc& d = b.desc[i];
+            _wire_off[i] = at;
+            uint8_t* f = _wire.p + at;
+            const uint64_t size = wsg_frame_size(d.opcode, d.mask, d.len, d.status);
+            const int hdr = wsg_header_pack(d.opcode, d.mask, d.len, d.status, 0, f);
+            const uint64_t prefix = size - uint64_t(hdr) - d.len;
+            if (prefix) {
+                f[hdr] = uint8_t((d.status >> 8) & 0xFF);
+                f[hdr + 1] = uint8_t(d.status & 0xFF);
+            }
+            if (d.len)
+                std::memcpy(f + hdr + prefix, b.payload.p + d.src_off, d.len);
+            at += size;
+        }
+        _wire_off[n] = at;
+    }
+    if (rc != WSG_OK) {
+        // nothing was handed out: the frames go back in front of anything
+        // queued meanwhile, so a later flush still sends them in order
+        std::scoped_lock locker(_lock);
+        const uint64_t shift = b.payload.len;
+        grow_pinned(b.payload.p, b.payload.cap, b.payload.len, b.payload.len + _q.payload.len);
+        if (_q.payload.len)
+            std::memcpy(b.payload.p + b.payload.len, _q.payload.p, _q.payload.len);
+        b.payload.len += _q.payload.len;
+        for (wsg_send_desc d : _q.desc) {
+            d.src_off += shift;
+            b.desc.push_back(d);
+        }
+        for (Rec& r : _q.recs)
+            b.recs.push_back(std::move(r));
+        std::swap(_q, b);
+        b.payload.len = 0;
+        b.desc.clear();
+        b.recs.clear();
+        check(rc, "wsg_encode_batch_host");
+    }
     size_t sent = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const uint8_t* f = _wire.p + _wire_off[i];
         const size_t len = size_t(_wire_off[i + 1] - _wire_off[i]);
-        if (recs[i].transport) {
-            recs[i].transport->SendAsync(f, len);
+        Rec rec;
+        {
+            std::scoped_lock locker(_lock);   // Forget() may run meanwhile
+            rec = b.recs[i];
+        }
+        if (rec.transport) {
+            rec.transport->SendAsync(f, len);
             ++sent;
-        } else if (recs[i].tag && sink) {
-            sink(user, recs[i].tag, f, len);
+        } else if (rec.deliver) {
+            (*rec.deliver)(f, len);
+            ++sent;
+        } else if (rec.tag && sink) {
+            sink(user, rec.tag, f, len);
             ++sent;
         }
     }
     return sent;
+}
+
+// ---------------------------------------------------------------- batch scope
+
+namespace {
+
+struct AutoState {
+    int depth = 0;
+    bool draining = false;
+    int enabled = -1;   // -1: from $WSG_AUTO_BATCH on first use
+    size_t max_frames = size_t(1) << 20;
+    uint64_t max_bytes = uint64_t(64) << 20;
+    WSReceiveBatch rx{nullptr};
+    WSSendBatch tx{nullptr};
+};
+
+AutoState& auto_state()
+{
+    thread_local AutoState st;
+    if (st.enabled < 0) {
+        const char* e = std::getenv("WSG_AUTO_BATCH");
+        st.enabled = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
+    }
+    return st;
+}
+
+} // namespace
+
+BatchScope::BatchScope() noexcept { ++auto_state().depth; }
+
+BatchScope::~BatchScope()
+{
+    AutoState& st = auto_state();
+    if (st.depth == 1 && !st.draining) {
+        try {
+            Flush();
+        } catch (...) {
+            // a destructor must not throw; the frames stay queued for the next flush
+        }
+    }
+    --st.depth;
+}
+
+size_t BatchScope::Flush()
+{
+    AutoState& st = auto_state();
+    if (st.draining)
+        return 0;
+    st.draining = true;
+    ++st.depth;   // callbacks' Send*Async queue into this thread's batch
+    struct Done {
+        AutoState& s;
+        ~Done()
+        {
+            --s.depth;
+            s.draining = false;
+        }
+    } done{st};
+    size_t n = 0;
+    // received frames first (their callbacks queue replies), then the sends;
+    // again while the callbacks keep queueing
+    for (int round = 0; round < 64 && (st.rx.frames() || st.tx.frames()); ++round) {
+        n += st.rx.Flush();
+        n += st.tx.Flush();
+    }
+    return n;
+}
+
+bool BatchScope::Enabled() { return auto_state().enabled != 0; }
+
+void BatchScope::SetEnabled(bool on) { auto_state().enabled = on ? 1 : 0; }
+
+bool BatchScope::Active()
+{
+    AutoState& st = auto_state();
+    return st.enabled != 0 && st.depth > 0;
+}
+
+void BatchScope::SetLimits(size_t frames, uint64_t bytes)
+{
+    AutoState& st = auto_state();
+    st.max_frames = std::max<size_t>(frames, 1);
+    st.max_bytes = std::max<uint64_t>(bytes, 1);
+}
+
+WSReceiveBatch& BatchScope::Receive() { return auto_state().rx; }
+
+WSSendBatch& BatchScope::Send() { return auto_state().tx; }
+
+void BatchScope::CheckLimits()
+{
+    AutoState& st = auto_state();
+    if (st.draining)
+        return;
+    if (st.rx.frames() >= st.max_frames || st.rx.bytes() >= st.max_bytes || st.tx.frames() >= st.max_frames ||
+        st.tx.payload_bytes() >= st.max_bytes)
+        Flush();
 }
 
 } // namespace WS

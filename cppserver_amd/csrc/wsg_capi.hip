@@ -30,7 +30,8 @@ struct wsg_ctx {
     int dec_blocks_per_cu = 48;   // k_decode grid: 40-56 best, 48 chosen (tools/tune.py: C2 -3.5 %, C3 ragged -2 % vs 32)
     int fan_waves_per_cu = 8;    // fan-out period path: waves per CU (tools/tune_enc.py CFG=c4: 8 best of 4-32)
     uint64_t small_avg = wsg::SMALL_AVG;   // batch encode: k_encode_small when wire_cap <= n * small_avg
-    unsigned long long* d_err = nullptr;
+    unsigned long long* d_err = nullptr;        // latch of the caller-visible async entry points (wsg_sync)
+    unsigned long long* d_err_host = nullptr;   // latch of the host-staged pipelines (their own status)
     // scratch
     wsg_enc_scratch enc;
     // staging for host entry points
@@ -254,6 +255,8 @@ int wsg_create(int device, wsg_ctx** out)
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_err, sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(c->d_err, 0xFF, sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->d_err_host, sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_err_host, 0xFF, sizeof(unsigned long long)) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess) {
         wsg_destroy(c);
         return WSG_EHIP;
@@ -296,6 +299,7 @@ int wsg_destroy(wsg_ctx* c)
         (void)hipEventDestroy(ev.b);
     }
     (void)hipFree(c->d_err);
+    (void)hipFree(c->d_err_host);
     free_enc(c->enc);
     (void)hipFree(c->d_stage);
     (void)hipFree(c->d_fs);
@@ -364,7 +368,7 @@ namespace {
 // Device decode: one k_decode launch (the pipelined host path runs several
 // of these concurrently, one per slot).
 int decode_launch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const uint64_t* d_frame_start, uint32_t n,
-                  uint8_t* d_out, wsg_recv_info* d_info, hipStream_t s)
+                  uint8_t* d_out, wsg_recv_info* d_info, hipStream_t s, unsigned long long* err)
 {
     if (n == 0) {
         if (wire_len && d_out != d_wire)
@@ -376,7 +380,7 @@ int decode_launch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const ui
     const uint64_t tiles = ceil_div(wire_len, wsg::TILE);
     const int t = timing_begin(c, s);
     WSG_HIP(wsg::launch_decode(s, grid_for(c, std::max(tiles, ceil_div(n, wsg::BLOCK)), c->dec_blocks_per_cu), d_wire, d_out, wire_len,
-                               d_frame_start, n, d_info, c->d_err));
+                               d_frame_start, n, d_info, err));
     timing_end(c, s, t);
     return WSG_OK;
 }
@@ -390,7 +394,7 @@ int wsg_decode_batch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const
         return WSG_EINVAL;
     if (!aligned16(d_wire) || !aligned16(d_out))
         return WSG_EINVAL;
-    return decode_launch(c, d_wire, wire_len, d_frame_start, n, d_out, d_info, pick(c, stream));
+    return decode_launch(c, d_wire, wire_len, d_frame_start, n, d_out, d_info, pick(c, stream), c->d_err);
 }
 
 namespace {
@@ -416,18 +420,19 @@ int ensure_enc(const wsg_ctx* c, wsg_enc_scratch& e, uint32_t n, uint64_t wire_c
 }
 
 int encode_launch(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, const wsg_send_desc* d_desc, uint32_t n,
-                  uint8_t* d_wire, uint64_t wire_cap, uint64_t* d_wire_off, wsg_enc_scratch& e)
+                  uint8_t* d_wire, uint64_t wire_cap, uint64_t* d_wire_off, wsg_enc_scratch& e,
+                  unsigned long long* err)
 {
     if (small_path(c, n, wire_cap)) {   // sizes scan, then one block per group of frames
         WSG_HIP(wsg::launch_encode_scan_small(s, d_desc, n, d_wire_off, e.d_scan));
         const int t = timing_begin(c, s);
-        WSG_HIP(wsg::launch_encode_small(s, d_payload, d_desc, n, d_wire_off, e.d_scan, d_wire, wire_cap, c->d_err));
+        WSG_HIP(wsg::launch_encode_small(s, d_payload, d_desc, n, d_wire_off, e.d_scan, d_wire, wire_cap, err));
         timing_end(c, s, t);
         return WSG_OK;
     }
     const uint64_t pieces_cap = pieces_bound(n, wire_cap);
     WSG_HIP(wsg::launch_encode_scan(s, d_desc, n, d_wire_off, e.d_piece_start, e.d_scan, e.d_piece_frame, pieces_cap,
-                                    wire_cap, c->d_err));
+                                    wire_cap, err));
     const int t = timing_begin(c, s);
     WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, ceil_div(pieces_cap, wsg::BLOCK / 64), c->enc_blocks_per_cu), d_payload, d_desc, n,
                                     d_wire_off, e.d_piece_start, e.d_piece_frame, d_wire, wire_cap));
@@ -451,7 +456,7 @@ int wsg_encode_batch(wsg_ctx* c, const uint8_t* d_payload, const wsg_send_desc* 
     }
     if (int rc = ensure_enc(c, c->enc, n, wire_cap))
         return rc;
-    return encode_launch(c, s, d_payload, d_desc, n, d_wire, wire_cap, d_wire_off, c->enc);
+    return encode_launch(c, s, d_payload, d_desc, n, d_wire, wire_cap, d_wire_off, c->enc, c->d_err);
 }
 
 namespace {
@@ -794,7 +799,7 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
         WSG_HIP(hipMemcpyAsync(sl.d_fs, sl.h_fs, m * sizeof(uint64_t), hipMemcpyHostToDevice, pp.h2d));
         if (int rc = pipe_to_kern(pp, sl))
             return rc;
-        if (int rc = decode_launch(c, sl.d_wire, len, sl.d_fs, m, sl.d_wire, sl.d_info, pp.kern))
+        if (int rc = decode_launch(c, sl.d_wire, len, sl.d_fs, m, sl.d_wire, sl.d_info, pp.kern, c->d_err_host))
             return rc;
         if (int rc = pipe_to_d2h(pp, sl))
             return rc;
@@ -819,7 +824,9 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
     for (auto& sl : c->slots)
         if (int rc = slot_drain(sl))
             return rc;
-    (void)wsg_sync(c, nullptr);   // clear the latch: segment-relative indices are not meaningful here
+    // the pipeline's kernels latched into d_err_host (segment-relative frame
+    // indices, meaningless to the caller); the status comes from the
+    // per-frame errors below, and the caller's own latch is left alone
 
     // batch semantics: a frame that runs into the next segment's first frame
     // overlaps it (EINVAL), it is not truncated; and the status is the error
@@ -836,6 +843,8 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
         if (r.error && !first)
             first = r.error;
     }
+    if (first)   // re-arm the pipeline's latch (every slot has drained)
+        WSG_HIP(hipMemset(c->d_err_host, 0xFF, sizeof(unsigned long long)));
     return first;
 }
 
@@ -985,7 +994,8 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
         if (int rc = pipe_to_kern(pp, sl))
             return rc;
         const uint64_t wlen = wire_off[g.i1] - wire_off[g.i0];
-        if (int rc = encode_launch(c, pp.kern, sl.d_payload, sl.d_desc, m, sl.d_wire, wlen, sl.d_woff, sl.enc))
+        if (int rc = encode_launch(c, pp.kern, sl.d_payload, sl.d_desc, m, sl.d_wire, wlen, sl.d_woff, sl.enc,
+                                   c->d_err_host))
             return rc;
         if (int rc = pipe_to_d2h(pp, sl))
             return rc;
@@ -1005,7 +1015,9 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
     for (auto& sl : c->slots)
         if (int rc = slot_drain(sl))
             return rc;
-    return wsg_sync(c, nullptr);   // capacity was checked above; anything latched is a real error
+    // the encode kernels latch only capacity errors, and capacity was checked
+    // on the host above: nothing for the pipeline's latch to report
+    return WSG_OK;
 }
 
 uint64_t wsg_frame_size(uint8_t opcode, int mask, uint64_t len, int32_t status)

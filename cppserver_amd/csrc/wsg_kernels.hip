@@ -95,8 +95,11 @@ __device__ __forceinline__ void st16nt(uint8_t* p, v4u v)
 #ifndef WSG_OUT_SC1
 #define WSG_OUT_SC1 0
 #endif
+#ifndef WSG_ENC_SC1
+#define WSG_ENC_SC1 0   // batch encode (piece kernel): write-through stores (A/B)
+#endif
 #ifndef WSG_FAN_SC1
-#define WSG_FAN_SC1 0   // fan-out period path: write-through stores (A/B)
+#define WSG_FAN_SC1 1   // fan-out period path: write-through (sc1) stores, 13.0 vs 14.3 us nontemporal at C4 (tools/tune_enc.py CFG=c4)
 #endif
 struct OutTile {
     uint8_t* p;   // tile base (wave-uniform)
@@ -878,11 +881,12 @@ struct Piece {
         if (!live)
             return;
         const uint32_t lane = threadIdx.x & 63;
+        const OutTile ot(wire + lo, uint32_t(PIECE), WSG_ENC_SC1 != 0);
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
             const uint64_t p = lo + (uint64_t(u) * 64 + lane) * CHUNK;
             if ((dmask >> u) & 1u) {
-                st16nt(wire + p, (s ? funnel(a[u], b[u], s) : a[u]) ^ kw);
+                ot.put(uint32_t(p - lo), (s ? funnel(a[u], b[u], s) : a[u]) ^ kw);
             } else if (p < hi && !(WSG_DIAG_ENC & 1)) {
                 edge_chunk(R, p, wire);   // header / status bytes, or a chunk shared with a neighbour
             }

@@ -15,8 +15,11 @@
  * every connection sees exactly the onWS* calls PrepareReceiveFrame would
  * have made, only later.
  *
- * Callback buffers are valid until the next Flush().  A batch is used from
- * one thread (the IO thread that owns the connections feeding it).
+ * Callback buffers are valid until the next Flush().  Feed / Clear / Forget
+ * may come from any thread (a mutex guards the queue, as the reference's
+ * per-session strands and locks let any IO thread call in); a Flush runs on
+ * the calling thread with that thread's GPU codec context unless the batch
+ * was given one, and fires the callbacks on that thread.
  */
 #ifndef CPPSERVER_AMD_WS_BATCH_H
 #define CPPSERVER_AMD_WS_BATCH_H
@@ -24,6 +27,9 @@
 #include "server/ws/ws.h"
 
 #include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 namespace CppServer {
@@ -51,8 +57,16 @@ public:
     //! inside a callback returns 0 (its frames go with the next one).
     size_t Flush();
 
-    size_t frames() const { return _cur.fs.size(); }
-    uint64_t bytes() const { return _cur.wire.len; }
+    size_t frames() const
+    {
+        std::scoped_lock l(_lock);
+        return _cur.fs.size();
+    }
+    uint64_t bytes() const
+    {
+        std::scoped_lock l(_lock);
+        return _cur.wire.len;
+    }
 
 private:
     struct Pinned {
@@ -70,11 +84,13 @@ private:
         std::vector<uint64_t> fs;
         std::vector<Rec> recs;
         std::vector<wsg_recv_info> info;
+        bool keyed = false;   // some frame carries a nonzero mask key: the GPU pass has bytes to change
         void reset()
         {
             wire.len = out.len = 0;
             fs.clear();
             recs.clear();
+            keyed = false;
         }
     };
 
@@ -85,6 +101,7 @@ private:
     wsg_ctx* _ctx;
     Batch _cur, _spare;
     bool _flushing = false;
+    mutable std::mutex _lock;   // _cur, the records of _spare, _flushing
 };
 
 class Transport;
@@ -117,6 +134,10 @@ public:
                int status = 0);
     //! The same, for a frame the flush sink receives with `tag`
     void Queue(void* tag, uint32_t key, uint8_t opcode, bool mask, const void* buffer, size_t size, int status = 0);
+    //! The same, for a frame handed to `deliver` at Flush() (a multicast:
+    //! encoded once, then copied to every session, ws_server.cpp:36-64)
+    void QueueFanout(std::function<void(const uint8_t* frame, size_t size)> deliver, uint32_t key, uint8_t opcode,
+                     bool mask, const void* buffer, size_t size, int status = 0);
     //! Drop every queued frame of `transport` (call before destroying it)
     void Forget(Transport& transport);
     //! Drop every queued frame queued with `tag`
@@ -125,8 +146,16 @@ public:
     //! returns the number of frames handed out
     size_t Flush(Sink sink = nullptr, void* user = nullptr);
 
-    size_t frames() const { return _desc.size(); }
-    uint64_t payload_bytes() const { return _payload.len; }
+    size_t frames() const
+    {
+        std::scoped_lock l(_lock);
+        return _q.desc.size();
+    }
+    uint64_t payload_bytes() const
+    {
+        std::scoped_lock l(_lock);
+        return _q.payload.len;
+    }
 
 private:
     struct Pinned {
@@ -136,16 +165,70 @@ private:
     struct Rec {
         Transport* transport;
         void* tag;
+        std::shared_ptr<std::function<void(const uint8_t*, size_t)>> deliver;
     };
-    void Push(Transport* t, void* tag, uint32_t key, uint8_t opcode, bool mask, const void* buffer, size_t size,
-              int status);
+    void Push(Rec rec, uint32_t key, uint8_t opcode, bool mask, const void* buffer, size_t size, int status);
+
+    struct Queue_ {
+        Pinned payload;
+        std::vector<wsg_send_desc> desc;
+        std::vector<Rec> recs;
+    };
 
     wsg_ctx* _ctx;
-    Pinned _payload, _wire;
-    std::vector<wsg_send_desc> _desc;
-    std::vector<Rec> _recs;
+    Queue_ _q, _inflight;   // frames being queued | the frames a flush is encoding
+    Pinned _wire;
     std::vector<uint64_t> _wire_off;
     bool _flushing = false;
+    mutable std::mutex _lock;   // _q, _flushing
+};
+
+/*
+ * Automatic batching: what makes the drop-in API fast without code changes.
+ *
+ * The reference encodes every Send*Async and unmasks every received frame on
+ * the spot, one connection at a time (ws.cpp:212-456).  Here
+ * WSClient/WSSession::onReceived open a BatchScope on the calling thread:
+ * the frames of the bytes read are framed on the host and unmasked in ONE
+ * GPU pass when the outermost scope closes, and every Send*Async made
+ * meanwhile — by the onWS* callbacks, e.g. an echo — is encoded in ONE GPU
+ * pass after them.  Callbacks still fire before onReceived returns, in
+ * arrival order, with the reference's arguments; each connection's frames
+ * leave in call order (a sync Send* / Receive* flushes first).
+ *
+ * A transport that reads many connections per loop iteration (an epoll /
+ * io_uring tick) opens one BatchScope around the iteration and every
+ * connection's frames of that tick share the two GPU passes.  A batch that
+ * reaches the limits (SetLimits) is flushed early.  Send*Async outside any
+ * scope (a timer thread, the multicaster of ws_multicast) is encoded per
+ * call.  $WSG_AUTO_BATCH=0 (or SetEnabled(false)) gives the per-call path.
+ */
+class BatchScope
+{
+public:
+    BatchScope() noexcept;
+    ~BatchScope();
+    BatchScope(const BatchScope&) = delete;
+    BatchScope& operator=(const BatchScope&) = delete;
+
+    //! Decode and deliver what this thread received, then encode and send
+    //! what it queued (repeated while the callbacks queue more); returns the
+    //! frames handled.  No effect from inside a delivery on this thread.
+    static size_t Flush();
+    //! Automatic batching on this thread (default: on, unless $WSG_AUTO_BATCH=0)
+    static bool Enabled();
+    static void SetEnabled(bool on);
+    //! Inside a scope on this thread
+    static bool Active();
+    //! Flush early when the receive batch holds `frames` frames or `bytes`
+    //! wire bytes, or the send batch that many frames / payload bytes
+    static void SetLimits(size_t frames, uint64_t bytes);
+
+    //! This thread's automatic batches (used by the WS classes)
+    static WSReceiveBatch& Receive();
+    static WSSendBatch& Send();
+    //! Early flush when a batch passed the limits (inside a scope)
+    static void CheckLimits();
 };
 
 } // namespace WS

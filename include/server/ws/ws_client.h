@@ -21,7 +21,7 @@ class WSClient : protected WebSocket
 {
 public:
     explicit WSClient(Transport& transport, wsg_ctx* codec = nullptr) : WebSocket(codec), _transport(transport) {}
-    virtual ~WSClient() = default;
+    virtual ~WSClient();
 
     //! Start the upgrade on a connected transport (reference WSClient::onConnected,
     //! ws_client.cpp:38-53): clear buffers, let onWSConnecting fill the
@@ -94,6 +94,7 @@ private:
     WSReceiveBatch* _rx_batch{nullptr};
     WSSendBatch* _tx_batch{nullptr};
     void ResetBuffers();
+    void RouteFrames(const void* buffer, size_t size);
     size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0);
     bool SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status = 0);
     bool ReceiveMessage(std::vector<uint8_t>& out);

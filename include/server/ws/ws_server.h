@@ -72,6 +72,8 @@ private:
 
     mutable std::shared_mutex _sessions_lock;
     std::vector<std::shared_ptr<WSSession>> _sessions;
+    // copy-on-write view of _sessions for batched multicast records
+    std::shared_ptr<const std::vector<std::shared_ptr<WSSession>>> _snapshot;
 };
 
 } // namespace WS

@@ -22,7 +22,7 @@ class WSSession : protected WebSocket
 
 public:
     explicit WSSession(Transport& transport, wsg_ctx* codec = nullptr) : WebSocket(codec), _transport(transport) {}
-    virtual ~WSSession() = default;
+    virtual ~WSSession();
 
     //! Accept a connected transport: clear buffers and wait for the client's
     //! upgrade request, answered through onReceived (PerformServerUpgrade,
@@ -93,6 +93,7 @@ private:
     WSReceiveBatch* _rx_batch{nullptr};
     WSSendBatch* _tx_batch{nullptr};
     void ResetBuffers();
+    void RouteFrames(const void* buffer, size_t size);
     size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0);
     bool SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status = 0);
     bool ReceiveMessage(std::vector<uint8_t>& out);

@@ -99,7 +99,9 @@ const char* wsg_strerror(int code);
  * d_out: wire_len bytes; on return it is the wire with every frame's payload
  * unmasked in place (ws.cpp:399-406); header and gap bytes are copied
  * unchanged.  d_out may equal d_wire (in-place).  d_info[i] describes frame i
- * (payload at d_out + d_info[i].payload_off).  d_wire/d_out 16-byte aligned. */
+ * (payload at d_out + d_info[i].payload_off).  d_wire/d_out 16-byte aligned;
+ * the kernel reads d_wire in whole 16-byte blocks, so the block holding the
+ * last wire byte must be readable (hipMalloc / torch allocations are).       */
 int wsg_decode_batch(wsg_ctx* ctx, const uint8_t* d_wire, uint64_t wire_len,
                      const uint64_t* d_frame_start, uint32_t n,
                      uint8_t* d_out, wsg_recv_info* d_info, void* stream);

@@ -19,6 +19,8 @@
 #include <memory>
 #include <random>
 #include <string>
+#include <thread>
+#include <cstring>
 #include <vector>
 
 using namespace CppServer::WS;
@@ -397,9 +399,9 @@ static void test_batched_send()
     p.client->messages.clear();
     p.session->SendTextAsync("a");
     p.session->SendText("b");
-    server.MulticastText("c");
+    server.MulticastText("c");   // batched too: one frame for every session at the flush
     p.session->SendTextAsync("d");
-    CHECK(server.FlushSend() == 1);
+    CHECK(server.FlushSend() == 2);
     p.pump();
     std::vector<std::string> got;
     for (auto& m : p.client->messages)
@@ -408,6 +410,128 @@ static void test_batched_send()
     for (auto& q : pairs)
         q->client->SetSendBatch(nullptr);
     server.EnableBatchSend(false);
+}
+
+// Automatic batching (ws_batch.h BatchScope): the drop-in path, no batch
+// set up by the user.  Sends inside a tick leave in one encode pass at its
+// end; a read's frames are unmasked in one pass and the echoes they trigger
+// go out in one more; messages and their order are the per-call path's.
+static void test_auto_batch_echo()
+{
+    for (int enabled = 1; enabled >= 0; --enabled) {
+        BatchScope::SetEnabled(enabled != 0);
+        Pair p;
+        std::vector<std::vector<uint8_t>> sent;
+        std::mt19937 gen(11 + enabled);
+        {
+            BatchScope tick;
+            for (int i = 0; i < 300; ++i) {
+                std::vector<uint8_t> m(gen() % 7 == 0 ? 70000 + gen() % 100 : gen() % 64);
+                for (auto& b : m)
+                    b = uint8_t(gen());
+                CHECK(p.client->SendBinaryAsync(m.data(), m.size()));
+                sent.push_back(m);
+            }
+            if (enabled)
+                CHECK(p.st.inbox.empty());   // queued until the tick ends
+        }
+        CHECK(!p.st.inbox.empty());
+        p.pump();
+        CHECK(p.client->messages == sent);
+        CHECK(p.session->last == sent.back());
+        // a sync send inside a tick flushes what the tick queued first
+        p.client->messages.clear();
+        {
+            BatchScope tick;
+            p.client->SendTextAsync("x");
+            p.client->SendText("y");
+            p.client->SendTextAsync("z");
+        }
+        p.pump();
+        std::vector<std::string> got;
+        for (auto& m : p.client->messages)
+            got.emplace_back(m.begin(), m.end());
+        CHECK(got == std::vector<std::string>({"x", "y", "z"}));
+    }
+    BatchScope::SetEnabled(true);
+}
+
+// ws_multicast's tick: `messages_rate` MulticastBinary calls in one scope are
+// encoded in one pass and reach every session registered at the call, in order.
+static void test_multicast_tick()
+{
+    WSServer server;
+    std::vector<std::unique_ptr<Pair>> pairs;
+    for (int i = 0; i < 5; ++i) {
+        pairs.emplace_back(new Pair());
+        pairs.back()->session->echo = false;
+        server.AddSession(pairs.back()->session);
+    }
+    std::vector<std::vector<uint8_t>> msgs;
+    {
+        BatchScope tick;
+        for (int i = 0; i < 10; ++i) {
+            std::vector<uint8_t> m(32, uint8_t(i));
+            msgs.push_back(m);
+            CHECK(server.MulticastBinary(m.data(), m.size()) == 1);
+        }
+        pairs.emplace_back(new Pair());   // joins after the calls: gets none of them
+        pairs.back()->session->echo = false;
+        server.AddSession(pairs.back()->session);
+        for (auto& p : pairs)
+            CHECK(p->ct.inbox.empty());
+    }
+    for (auto& p : pairs)
+        p->pump();
+    for (size_t i = 0; i + 1 < pairs.size(); ++i)
+        CHECK(pairs[i]->client->messages == msgs);
+    CHECK(pairs.back()->client->messages.empty());
+}
+
+// One explicit send batch fed from several threads at once (a WSServer's
+// sessions on different IO threads), flushed from yet another.
+static void test_batch_threads()
+{
+    WSSendBatch batch;
+    const int T = 4, N = 2000;
+    std::vector<std::thread> th;
+    std::vector<int> tags(T);
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t]() {
+            for (int i = 0; i < N; ++i) {
+                const uint32_t v = uint32_t(t * N + i);
+                batch.Queue(&tags[t], 0x01020304u, WSG_FIN | WSG_BINARY, true, &v, sizeof(v));
+            }
+        });
+    size_t flushed = 0;
+    struct Count {
+        std::vector<uint32_t> last;
+        size_t n = 0;
+        bool ordered = true;
+        int* base;
+    } cnt{std::vector<uint32_t>(T, 0), 0, true, tags.data()};
+    auto sink = [](void* user, void* tag, const uint8_t* f, size_t len) {
+        Count* c = static_cast<Count*>(user);
+        const int t = int(static_cast<int*>(tag) - c->base);
+        uint32_t v;
+        std::memcpy(&v, f + len - 4, 4);
+        const uint8_t k[4] = {4, 3, 2, 1};
+        uint8_t* b = reinterpret_cast<uint8_t*>(&v);
+        for (int j = 0; j < 4; ++j)
+            b[j] ^= k[j];   // unmask (key bytes little-endian, ws.cpp:244-247)
+        if (c->last[size_t(t)] && v <= c->last[size_t(t)])
+            c->ordered = false;
+        c->last[size_t(t)] = v;
+        ++c->n;
+    };
+    for (int round = 0; round < 50; ++round)
+        flushed += batch.Flush(sink, &cnt);
+    for (auto& x : th)
+        x.join();
+    flushed += batch.Flush(sink, &cnt);
+    CHECK(flushed == size_t(T) * N);
+    CHECK(cnt.n == size_t(T) * N);
+    CHECK(cnt.ordered);
 }
 
 // WSS (reference include/server/ws/wss_*.h): the same codec over a transport
@@ -501,6 +625,9 @@ int main()
         test_soak();
         test_batched_server_receive();
         test_batched_send();
+        test_auto_batch_echo();
+        test_multicast_tick();
+        test_batch_threads();
         test_wss();
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());

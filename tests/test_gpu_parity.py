@@ -574,6 +574,30 @@ def test_decode_batch_host_segmented(codec, stage_mb, monkeypatch):
                 assert np.array_equal(info[fld], info_o[fld]), (variant, pinned, fld)
 
 
+def test_host_pipeline_keeps_caller_latch(codec):
+    """A host-staged call between an async batch call and its wsg_sync must
+    not clear (or add to) the error that async call latched."""
+    frame = bytes([0x82, 0x05, 1, 2, 3, 4, 5])
+    bad = np.frombuffer(frame + frame[:4], dtype=np.uint8)   # the second frame runs past the wire
+    w = dev(bad)
+    f = dev(np.array([0, 7], dtype=np.int64))
+    codec.decode_batch(w, f)                                  # async: latches ETRUNC
+    wire, fs, _ = wl.c2_wire(8, 1000, seed=3)
+    rc, _, _ = codec.decode_batch_host(wire, fs)              # a clean host-staged batch
+    assert rc == 0
+    rc2, _, _ = codec.decode_batch_host(bad, np.array([0, 7], np.uint64))   # its own error, its own status
+    assert rc2 == ca.WSG_ETRUNC
+    assert codec.sync_status() == ca.WSG_ETRUNC               # the async call's error is still there
+    assert codec.sync_status() == 0
+
+
+def test_encode_wire_cap_checked(codec):
+    wire = torch.empty(64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(ca.WSGError):
+        codec.encode_batch(dev(np.zeros(16, np.uint8)), ca.desc_to_tensor(np.zeros(1, dtype=SEND_DESC), "cuda"),
+                           wire=wire, wire_cap=128)
+
+
 def test_timing_hook_counts_launches(codec):
     wire, fs, _ = wl.c2_wire(64, 65536, seed=10)
     w, f = dev(wire), dev(fs.view(np.int64))
