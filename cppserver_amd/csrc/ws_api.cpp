@@ -83,6 +83,19 @@ bool WSClient::Connect()
     return _transport.Send(req.data(), req.size()) == req.size();
 }
 
+bool WSClient::ConnectAsync()
+{
+    if (!_transport.IsConnected())
+        return false;
+    ResetBuffers();
+    _http_buf.clear();
+    HTTP::HTTPRequest request;
+    onWSConnecting(request);
+    request.SetBody();
+    const std::string& req = request.cache();
+    return _transport.SendAsync(req.data(), req.size());
+}
+
 bool WSClient::Disconnect()
 {
     const bool ok = _transport.Disconnect();
@@ -146,7 +159,8 @@ void WSClient::SetSendBatch(WSSendBatch* batch)
     _tx_batch = batch;
 }
 
-size_t WSClient::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status)
+size_t WSClient::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status,
+                           const CppCommon::Timespan* timeout)
 {
     if (_tx_batch)
         _tx_batch->Flush();   // earlier async frames go first
@@ -154,7 +168,8 @@ size_t WSClient::SendFrame(uint8_t opcode, const void* buffer, size_t size, int 
         BatchScope::Send().Flush();
     std::scoped_lock locker(_ws_send_lock);
     PrepareSendFrame(opcode, true, buffer, size, status);
-    return _transport.Send(_ws_send_buffer.data(), _ws_send_buffer.size());
+    return timeout ? _transport.Send(_ws_send_buffer.data(), _ws_send_buffer.size(), *timeout)
+                   : _transport.Send(_ws_send_buffer.data(), _ws_send_buffer.size());
 }
 
 bool WSClient::SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status)
@@ -175,7 +190,7 @@ bool WSClient::SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, i
     return true;
 }
 
-bool WSClient::ReceiveMessage(std::vector<uint8_t>& out)
+bool WSClient::ReceiveMessage(std::vector<uint8_t>& out, const CppCommon::Timespan* timeout)
 {
     if (!_ws_handshaked)
         return false;
@@ -184,8 +199,10 @@ bool WSClient::ReceiveMessage(std::vector<uint8_t>& out)
     return receive_message(
         out, [this]() { return RequiredReceiveFrameSize(); },
         [this](const void* b, size_t n) { PrepareReceiveFrame(b, n); },
-        [this](void* b, size_t n) { return _transport.Receive(b, n); }, _ws_receive_final_buffer,
-        _ws_frame_received, _ws_final_received);
+        [this, timeout](void* b, size_t n) {
+            return timeout ? _transport.Receive(b, n, *timeout) : _transport.Receive(b, n);
+        },
+        _ws_receive_final_buffer, _ws_frame_received, _ws_final_received);
 }
 
 std::string WSClient::ReceiveText()
@@ -196,10 +213,25 @@ std::string WSClient::ReceiveText()
     return std::string(msg.begin(), msg.end());
 }
 
+std::string WSClient::ReceiveText(const CppCommon::Timespan& timeout)
+{
+    std::vector<uint8_t> msg;
+    if (!ReceiveMessage(msg, &timeout))
+        return std::string();
+    return std::string(msg.begin(), msg.end());
+}
+
 std::vector<uint8_t> WSClient::ReceiveBinary()
 {
     std::vector<uint8_t> msg;
     ReceiveMessage(msg);
+    return msg;
+}
+
+std::vector<uint8_t> WSClient::ReceiveBinary(const CppCommon::Timespan& timeout)
+{
+    std::vector<uint8_t> msg;
+    ReceiveMessage(msg, &timeout);
     return msg;
 }
 
@@ -300,7 +332,8 @@ void WSSession::SetSendBatch(WSSendBatch* batch)
     _tx_batch = batch;
 }
 
-size_t WSSession::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status)
+size_t WSSession::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status,
+                            const CppCommon::Timespan* timeout)
 {
     if (_tx_batch)
         _tx_batch->Flush();   // earlier async frames go first
@@ -308,7 +341,8 @@ size_t WSSession::SendFrame(uint8_t opcode, const void* buffer, size_t size, int
         BatchScope::Send().Flush();
     std::scoped_lock locker(_ws_send_lock);
     PrepareSendFrame(opcode, false, buffer, size, status);
-    return _transport.Send(_ws_send_buffer.data(), _ws_send_buffer.size());
+    return timeout ? _transport.Send(_ws_send_buffer.data(), _ws_send_buffer.size(), *timeout)
+                   : _transport.Send(_ws_send_buffer.data(), _ws_send_buffer.size());
 }
 
 bool WSSession::SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status)
@@ -329,7 +363,7 @@ bool WSSession::SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, 
     return true;
 }
 
-bool WSSession::ReceiveMessage(std::vector<uint8_t>& out)
+bool WSSession::ReceiveMessage(std::vector<uint8_t>& out, const CppCommon::Timespan* timeout)
 {
     if (!_ws_handshaked)
         return false;
@@ -338,8 +372,10 @@ bool WSSession::ReceiveMessage(std::vector<uint8_t>& out)
     return receive_message(
         out, [this]() { return RequiredReceiveFrameSize(); },
         [this](const void* b, size_t n) { PrepareReceiveFrame(b, n); },
-        [this](void* b, size_t n) { return _transport.Receive(b, n); }, _ws_receive_final_buffer,
-        _ws_frame_received, _ws_final_received);
+        [this, timeout](void* b, size_t n) {
+            return timeout ? _transport.Receive(b, n, *timeout) : _transport.Receive(b, n);
+        },
+        _ws_receive_final_buffer, _ws_frame_received, _ws_final_received);
 }
 
 std::string WSSession::ReceiveText()
@@ -350,10 +386,25 @@ std::string WSSession::ReceiveText()
     return std::string(msg.begin(), msg.end());
 }
 
+std::string WSSession::ReceiveText(const CppCommon::Timespan& timeout)
+{
+    std::vector<uint8_t> msg;
+    if (!ReceiveMessage(msg, &timeout))
+        return std::string();
+    return std::string(msg.begin(), msg.end());
+}
+
 std::vector<uint8_t> WSSession::ReceiveBinary()
 {
     std::vector<uint8_t> msg;
     ReceiveMessage(msg);
+    return msg;
+}
+
+std::vector<uint8_t> WSSession::ReceiveBinary(const CppCommon::Timespan& timeout)
+{
+    std::vector<uint8_t> msg;
+    ReceiveMessage(msg, &timeout);
     return msg;
 }
 

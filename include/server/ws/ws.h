@@ -13,13 +13,15 @@
  * PerformClientUpgrade / PerformServerUpgrade over the HTTP request/response
  * subset of include/server/http/, with the reference's onWSConnecting /
  * onWSConnected hooks.  The reference's client variant also takes the
- * connection's UUID, which it does not use; it is dropped here.
+ * connection's UUID (ws.h:62), which its body does not use; both forms are
+ * here.
  */
 #ifndef CPPSERVER_AMD_WS_H
 #define CPPSERVER_AMD_WS_H
 
 #include "wsg_capi.h"
 #include "server/http/http_request.h"
+#include "server/ws/ws_common.h"
 #include "server/http/http_response.h"
 
 #include <array>
@@ -79,6 +81,12 @@ public:
     //! Sec-WebSocket-Accept digest of this connection's nonce.  On success
     //! the connection is handshaked with a random send key, onWSConnected(response).
     bool PerformClientUpgrade(const HTTP::HTTPResponse& response);
+    //! The reference's signature (ws.h:62): the connection id is not used
+    bool PerformClientUpgrade(const HTTP::HTTPResponse& response, const CppCommon::UUID& id)
+    {
+        (void)id;
+        return PerformClientUpgrade(response);
+    }
     //! Answer a client's upgrade request (reference ws.cpp:103-210): validate
     //! it, build the 101 response (or a 400 error), let onWSConnecting veto
     //! it, SendResponse(), handshake with send key 0, onWSConnected(request).

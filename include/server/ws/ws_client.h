@@ -4,8 +4,10 @@
  * Same Send, Close and Receive surface as the reference WSClient
  * (include/server/ws/ws_client.h:39-96): every send locks _ws_send_lock,
  * encodes with mask = true and the connection's random key, and hands the
- * frame to the transport.  Timeout overloads (CppCommon::Timespan) are not
- * carried over: timeouts belong to the transport.
+ * frame to the transport.  The timeout overloads (CppCommon::Timespan,
+ * server/ws/ws_common.h) pass the timeout to the transport's Send / Receive.
+ * Connect(resolver) / ConnectAsync(resolver) take an Asio resolver in the
+ * reference; name resolution belongs to the transport here.
  */
 #ifndef CPPSERVER_AMD_WS_CLIENT_H
 #define CPPSERVER_AMD_WS_CLIENT_H
@@ -28,6 +30,9 @@ public:
     //! request, send it.  The connection is handshaked when the server's 101
     //! response arrives through onReceived (PerformClientUpgrade).
     virtual bool Connect();
+    //! As Connect, with the upgrade request queued on the transport
+    //! (reference ws_client.cpp:22-30: HTTPClient::ConnectAsync, then onConnected)
+    virtual bool ConnectAsync();
     virtual bool Disconnect();
     bool IsConnected() const { return _transport.IsConnected() && _ws_handshaked; }
 
@@ -42,32 +47,44 @@ public:
 
     size_t SendText(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_TEXT, buffer, size); }
     size_t SendText(std::string_view text) { return SendFrame(WS_FIN | WS_TEXT, text.data(), text.size()); }
+    size_t SendText(const void* buffer, size_t size, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_TEXT, buffer, size, 0, &timeout); }
+    size_t SendText(std::string_view text, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_TEXT, text.data(), text.size(), 0, &timeout); }
     bool SendTextAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_TEXT, buffer, size); }
     bool SendTextAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_TEXT, text.data(), text.size()); }
 
     size_t SendBinary(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_BINARY, buffer, size); }
     size_t SendBinary(std::string_view text) { return SendFrame(WS_FIN | WS_BINARY, text.data(), text.size()); }
+    size_t SendBinary(const void* buffer, size_t size, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_BINARY, buffer, size, 0, &timeout); }
+    size_t SendBinary(std::string_view text, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_BINARY, text.data(), text.size(), 0, &timeout); }
     bool SendBinaryAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_BINARY, buffer, size); }
     bool SendBinaryAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_BINARY, text.data(), text.size()); }
 
     size_t SendClose(int status, const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_CLOSE, buffer, size, status); }
     size_t SendClose(int status, std::string_view text) { return SendFrame(WS_FIN | WS_CLOSE, text.data(), text.size(), status); }
+    size_t SendClose(int status, const void* buffer, size_t size, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_CLOSE, buffer, size, status, &timeout); }
+    size_t SendClose(int status, std::string_view text, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_CLOSE, text.data(), text.size(), status, &timeout); }
     bool SendCloseAsync(int status, const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_CLOSE, buffer, size, status); }
     bool SendCloseAsync(int status, std::string_view text) { return SendFrameAsync(WS_FIN | WS_CLOSE, text.data(), text.size(), status); }
 
     size_t SendPing(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_PING, buffer, size); }
     size_t SendPing(std::string_view text) { return SendFrame(WS_FIN | WS_PING, text.data(), text.size()); }
+    size_t SendPing(const void* buffer, size_t size, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_PING, buffer, size, 0, &timeout); }
+    size_t SendPing(std::string_view text, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_PING, text.data(), text.size(), 0, &timeout); }
     bool SendPingAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_PING, buffer, size); }
     bool SendPingAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_PING, text.data(), text.size()); }
 
     size_t SendPong(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_PONG, buffer, size); }
     size_t SendPong(std::string_view text) { return SendFrame(WS_FIN | WS_PONG, text.data(), text.size()); }
+    size_t SendPong(const void* buffer, size_t size, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_PONG, buffer, size, 0, &timeout); }
+    size_t SendPong(std::string_view text, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_PONG, text.data(), text.size(), 0, &timeout); }
     bool SendPongAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_PONG, buffer, size); }
     bool SendPongAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_PONG, text.data(), text.size()); }
 
     //! Synchronous receive of one message (reference ws_client.cpp:129-251).
     std::string ReceiveText();
+    std::string ReceiveText(const CppCommon::Timespan& timeout);
     std::vector<uint8_t> ReceiveBinary();
+    std::vector<uint8_t> ReceiveBinary(const CppCommon::Timespan& timeout);
 
     //! Bytes read by the transport (the reference's TCPClient::onReceived override)
     void onReceived(const void* buffer, size_t size);
@@ -95,9 +112,10 @@ private:
     WSSendBatch* _tx_batch{nullptr};
     void ResetBuffers();
     void RouteFrames(const void* buffer, size_t size);
-    size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0);
+    size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0,
+                     const CppCommon::Timespan* timeout = nullptr);
     bool SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status = 0);
-    bool ReceiveMessage(std::vector<uint8_t>& out);
+    bool ReceiveMessage(std::vector<uint8_t>& out, const CppCommon::Timespan* timeout = nullptr);
 };
 
 } // namespace WS

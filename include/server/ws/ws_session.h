@@ -38,31 +38,43 @@ public:
 
     size_t SendText(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_TEXT, buffer, size); }
     size_t SendText(std::string_view text) { return SendFrame(WS_FIN | WS_TEXT, text.data(), text.size()); }
+    size_t SendText(const void* buffer, size_t size, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_TEXT, buffer, size, 0, &timeout); }
+    size_t SendText(std::string_view text, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_TEXT, text.data(), text.size(), 0, &timeout); }
     bool SendTextAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_TEXT, buffer, size); }
     bool SendTextAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_TEXT, text.data(), text.size()); }
 
     size_t SendBinary(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_BINARY, buffer, size); }
     size_t SendBinary(std::string_view text) { return SendFrame(WS_FIN | WS_BINARY, text.data(), text.size()); }
+    size_t SendBinary(const void* buffer, size_t size, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_BINARY, buffer, size, 0, &timeout); }
+    size_t SendBinary(std::string_view text, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_BINARY, text.data(), text.size(), 0, &timeout); }
     bool SendBinaryAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_BINARY, buffer, size); }
     bool SendBinaryAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_BINARY, text.data(), text.size()); }
 
     size_t SendClose(int status, const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_CLOSE, buffer, size, status); }
     size_t SendClose(int status, std::string_view text) { return SendFrame(WS_FIN | WS_CLOSE, text.data(), text.size(), status); }
+    size_t SendClose(int status, const void* buffer, size_t size, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_CLOSE, buffer, size, status, &timeout); }
+    size_t SendClose(int status, std::string_view text, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_CLOSE, text.data(), text.size(), status, &timeout); }
     bool SendCloseAsync(int status, const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_CLOSE, buffer, size, status); }
     bool SendCloseAsync(int status, std::string_view text) { return SendFrameAsync(WS_FIN | WS_CLOSE, text.data(), text.size(), status); }
 
     size_t SendPing(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_PING, buffer, size); }
     size_t SendPing(std::string_view text) { return SendFrame(WS_FIN | WS_PING, text.data(), text.size()); }
+    size_t SendPing(const void* buffer, size_t size, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_PING, buffer, size, 0, &timeout); }
+    size_t SendPing(std::string_view text, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_PING, text.data(), text.size(), 0, &timeout); }
     bool SendPingAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_PING, buffer, size); }
     bool SendPingAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_PING, text.data(), text.size()); }
 
     size_t SendPong(const void* buffer, size_t size) { return SendFrame(WS_FIN | WS_PONG, buffer, size); }
     size_t SendPong(std::string_view text) { return SendFrame(WS_FIN | WS_PONG, text.data(), text.size()); }
+    size_t SendPong(const void* buffer, size_t size, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_PONG, buffer, size, 0, &timeout); }
+    size_t SendPong(std::string_view text, const CppCommon::Timespan& timeout) { return SendFrame(WS_FIN | WS_PONG, text.data(), text.size(), 0, &timeout); }
     bool SendPongAsync(const void* buffer, size_t size) { return SendFrameAsync(WS_FIN | WS_PONG, buffer, size); }
     bool SendPongAsync(std::string_view text) { return SendFrameAsync(WS_FIN | WS_PONG, text.data(), text.size()); }
 
     std::string ReceiveText();
+    std::string ReceiveText(const CppCommon::Timespan& timeout);
     std::vector<uint8_t> ReceiveBinary();
+    std::vector<uint8_t> ReceiveBinary(const CppCommon::Timespan& timeout);
 
     //! Bytes read by the transport (reference ws_session.cpp:40-51).  With a
     //! receive batch set they are framed into the batch, and the onWS*
@@ -94,9 +106,10 @@ private:
     WSSendBatch* _tx_batch{nullptr};
     void ResetBuffers();
     void RouteFrames(const void* buffer, size_t size);
-    size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0);
+    size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0,
+                     const CppCommon::Timespan* timeout = nullptr);
     bool SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status = 0);
-    bool ReceiveMessage(std::vector<uint8_t>& out);
+    bool ReceiveMessage(std::vector<uint8_t>& out, const CppCommon::Timespan* timeout = nullptr);
 };
 
 } // namespace WS

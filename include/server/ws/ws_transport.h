@@ -11,6 +11,8 @@
 #ifndef CPPSERVER_AMD_WS_TRANSPORT_H
 #define CPPSERVER_AMD_WS_TRANSPORT_H
 
+#include "server/ws/ws_common.h"
+
 #include <cstddef>
 
 namespace CppServer {
@@ -26,6 +28,18 @@ public:
     virtual bool SendAsync(const void* buffer, size_t size) = 0;
     //! Blocking receive of up to size bytes (TCPClient::Receive)
     virtual size_t Receive(void* buffer, size_t size) = 0;
+    //! The same with a timeout (TCPClient::Send / Receive(..., timeout)); a
+    //! transport without timeouts of its own may keep these defaults
+    virtual size_t Send(const void* buffer, size_t size, const CppCommon::Timespan& timeout)
+    {
+        (void)timeout;
+        return Send(buffer, size);
+    }
+    virtual size_t Receive(void* buffer, size_t size, const CppCommon::Timespan& timeout)
+    {
+        (void)timeout;
+        return Receive(buffer, size);
+    }
     virtual bool Disconnect() = 0;
     virtual bool IsConnected() const = 0;
 };

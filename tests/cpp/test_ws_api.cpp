@@ -236,6 +236,38 @@ static void test_sync_receive()
     }
     p.session->SendText("hello");
     CHECK(p.client->ReceiveText() == "hello");
+    // the reference's timeout overloads (ws_client.h:55-96, ws_session.h:48-89)
+    const CppCommon::Timespan t = CppCommon::Timespan::seconds(1);
+    CHECK(p.client->SendText("with timeout", t) == 6 + 12);
+    CHECK(p.session->ReceiveText(t) == "with timeout");
+    CHECK(p.session->SendBinary("xy", 2, t) == 2 + 2);
+    CHECK(p.client->ReceiveBinary(t) == std::vector<uint8_t>({'x', 'y'}));
+}
+
+// ConnectAsync (reference ws_client.h:41): the upgrade request is queued on
+// the transport; the 101 response completes it through onReceived
+static void test_connect_async()
+{
+    Loopback ct, st;
+    ct.peer = &st;
+    st.peer = &ct;
+    EchoClient client(ct);
+    EchoSession session(st);
+    session.Connect();
+    CHECK(client.ConnectAsync());
+    for (int i = 0; i < 4; ++i) {
+        if (!st.inbox.empty()) {
+            std::vector<uint8_t> b(st.inbox.begin(), st.inbox.end());
+            st.inbox.clear();
+            session.onReceived(b.data(), b.size());
+        }
+        if (!ct.inbox.empty()) {
+            std::vector<uint8_t> b(ct.inbox.begin(), ct.inbox.end());
+            ct.inbox.clear();
+            client.onReceived(b.data(), b.size());
+        }
+    }
+    CHECK(client.connected && client.IsConnected());
 }
 
 static void test_soak()
@@ -622,6 +654,7 @@ int main()
         test_multicast();
         test_ping_pong_and_close();
         test_sync_receive();
+        test_connect_async();
         test_soak();
         test_batched_server_receive();
         test_batched_send();
