@@ -62,6 +62,9 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_DEC_RELOAD
 #define WSG_DEC_RELOAD 1   // k_decode staged tiles re-read their bytes instead of holding them in registers
 #endif
+#ifndef WSG_DEC_INFO_LAST
+#define WSG_DEC_INFO_LAST 0   // k_decode: per-frame info slice after the tiles, on the grid's last blocks (A/B)
+#endif
 #ifndef WSG_FAN_PERIOD
 #define WSG_FAN_PERIOD 1   // fan-out: period path (k_fanout_period) where the frame size allows; 0 = flat kernel only
 #endif
@@ -87,11 +90,12 @@ __device__ __forceinline__ void st16nt(uint8_t* p, v4u v)
 }
 
 // Stores of a once-written output stream.  Write-through (sc1) buffer stores
-// beat nontemporal ones in tools/membench.hip's copy (C2 footprint: 83.8-83.9
+// beat nontemporal ones in tools/membench.hip's copy (C2 footprint: 83.4-83.9
 // vs 85.0-85.5 us) and write-only stream (43.6 vs 47.4 us), but NOT in
 // k_decode: 90.7 vs 87.9 us on C2 and 0.825 vs 0.782 ms on C3's ragged
-// frames (tools/tune.py, same box, interleaved), so decode keeps nontemporal
-// stores; WSG_OUT_SC1=1 builds the write-through variant for A/B runs.
+// frames, and 90.1 vs 86.3 us with buffer loads too (tools/tune.py, same box,
+// interleaved, two boxes), so decode keeps nontemporal stores; the fan-out
+// (write-only) takes them.  WSG_OUT_SC1=1 builds the decode variant for A/B.
 #ifndef WSG_OUT_SC1
 #define WSG_OUT_SC1 0
 #endif
@@ -483,19 +487,26 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
                                                   uint32_t stride, wsg_recv_info* __restrict__ info,
                                                   unsigned long long* err, uint64_t num_tiles)
 {
-    // per-frame slice: header unpack + checks, one lane per frame
-    const uint64_t fstride = uint64_t(gridDim.x) * BLOCK;
-    for (uint64_t i0 = uint64_t(blockIdx.x) * BLOCK + (threadIdx.x & ~63u); i0 < n && !WSG_DIAG_NOINFO;
-         i0 += fstride) {
-        const uint64_t i = i0 + (threadIdx.x & 63u);
-        if (i < n) {
-            wsg_recv_info r;
-            const int e = frame_parse(wire, wire_len, fs[i], i + 1 < n ? fs[i + 1] : wire_len, r);
-            if (e != 0)
-                atomicMin(err, (static_cast<unsigned long long>(i) << 8) | static_cast<unsigned long long>(-e));
-            store_info(info + i, r);
+    // per-frame slice: header unpack + checks, one lane per frame.
+    // WSG_DEC_INFO_LAST: run by the grid's last blocks after their tiles
+    // (the first blocks of a grid smaller than the tile count stream two
+    // tiles each, so frames there would lengthen the longest blocks)
+    auto info_slice = [&]() {
+        const uint64_t fstride = uint64_t(gridDim.x) * BLOCK;
+        const uint64_t vb = WSG_DEC_INFO_LAST ? uint64_t(gridDim.x - 1 - blockIdx.x) : uint64_t(blockIdx.x);
+        for (uint64_t i0 = vb * BLOCK + (threadIdx.x & ~63u); i0 < n && !WSG_DIAG_NOINFO; i0 += fstride) {
+            const uint64_t i = i0 + (threadIdx.x & 63u);
+            if (i < n) {
+                wsg_recv_info r;
+                const int e = frame_parse(wire, wire_len, fs[i], i + 1 < n ? fs[i + 1] : wire_len, r);
+                if (e != 0)
+                    atomicMin(err, (static_cast<unsigned long long>(i) << 8) | static_cast<unsigned long long>(-e));
+                store_info(info + i, r);
+            }
         }
-    }
+    };
+    if (!WSG_DEC_INFO_LAST)
+        info_slice();
 
     for (uint64_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
         const uint64_t base = t * TILE;
@@ -699,6 +710,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
             }
         }
     }
+    if (WSG_DEC_INFO_LAST)
+        info_slice();
 }
 
 // ===========================================================================
