@@ -171,6 +171,7 @@ void WSReceiveBatch::Forget(WebSocket& ws)
         for (Rec& r : b->recs)
             if (r.ws == &ws)
                 r.ws = nullptr;
+    _forgets.fetch_add(1, std::memory_order_release);
 }
 
 size_t WSReceiveBatch::Flush()
@@ -221,10 +222,16 @@ size_t WSReceiveBatch::Flush()
         }
     }
     size_t delivered = 0;
-    for (size_t r = 0; r < b.recs.size(); ++r) {
-        Rec rec;
-        {
-            std::scoped_lock locker(_lock);   // a callback / another thread may Forget() a connection
+    // the records as of the swap; a Forget() (a callback dropping a
+    // connection) makes the rest be re-read under the lock
+    const std::vector<Rec> snap = b.recs;
+    uint64_t seen = _forgets.load(std::memory_order_acquire);
+    bool relock = false;
+    for (size_t r = 0; r < snap.size(); ++r) {
+        Rec rec = snap[r];
+        if (relock || _forgets.load(std::memory_order_acquire) != seen) {
+            relock = true;
+            std::scoped_lock locker(_lock);
             rec = b.recs[r];
         }
         if (!rec.ws)
@@ -320,6 +327,7 @@ void WSSendBatch::Forget(Transport& transport)
         for (Rec& r : q->recs)
             if (r.transport == &transport)
                 r = Rec{nullptr, nullptr, nullptr};
+    _forgets.fetch_add(1, std::memory_order_release);
 }
 
 void WSSendBatch::Forget(void* tag)
@@ -329,6 +337,7 @@ void WSSendBatch::Forget(void* tag)
         for (Rec& r : q->recs)
             if (r.tag == tag && !r.transport)
                 r = Rec{nullptr, nullptr, nullptr};
+    _forgets.fetch_add(1, std::memory_order_release);
 }
 
 size_t WSSendBatch::Flush(Sink sink, void* user)
@@ -413,13 +422,20 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
         check(rc, "wsg_encode_batch_host");
     }
     size_t sent = 0;
+    // records as of the swap; after a Forget() the rest are re-read under the lock
+    const uint64_t seen = _forgets.load(std::memory_order_acquire);
+    bool relock = false;
     for (uint32_t i = 0; i < n; ++i) {
         const uint8_t* f = _wire.p + _wire_off[i];
         const size_t len = size_t(_wire_off[i + 1] - _wire_off[i]);
+        const Rec* rp = &b.recs[i];   // only this flush writes b.recs' length; Forget() writes entries
         Rec rec;
-        {
-            std::scoped_lock locker(_lock);   // Forget() may run meanwhile
-            rec = b.recs[i];
+        if (relock || _forgets.load(std::memory_order_acquire) != seen) {
+            relock = true;
+            std::scoped_lock locker(_lock);
+            rec = *rp;
+        } else {
+            rec = *rp;
         }
         if (rec.transport) {
             rec.transport->SendAsync(f, len);

@@ -26,6 +26,7 @@
 
 #include "server/ws/ws.h"
 
+#include <atomic>
 #include <cstdint>
 #include <functional>
 #include <memory>
@@ -102,6 +103,7 @@ private:
     Batch _cur, _spare;
     bool _flushing = false;
     mutable std::mutex _lock;   // _cur, the records of _spare, _flushing
+    std::atomic<uint64_t> _forgets{0};   // Forget() calls: a flush re-reads its records after one
 };
 
 class Transport;
@@ -181,6 +183,7 @@ private:
     std::vector<uint64_t> _wire_off;
     bool _flushing = false;
     mutable std::mutex _lock;   // _q, _flushing
+    std::atomic<uint64_t> _forgets{0};   // Forget() calls: a flush re-reads its records after one
 };
 
 /*
