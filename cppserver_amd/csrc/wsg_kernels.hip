@@ -1508,7 +1508,9 @@ __global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict_
     const uint64_t chunks = (total + CHUNK - 1) / CHUNK;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wpb = blockDim.x / 64;              // 1, 2 or 4 waves per block (host: W % wpb == 0)
-    const uint64_t row0 = (uint64_t(blockIdx.x) * wpb + threadIdx.x / 64) * 64;
+    // wave-uniform (readfirstlane): the write-through stores' buffer resource
+    // must sit in SGPRs, or every store becomes a waterfall loop
+    const uint64_t row0 = (uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x / 64)) * 64;
     const uint64_t rstep = uint64_t(gridDim.x) * wpb * 64;   // W rows: a multiple of G (dm groups)
     if (row0 >= chunks)
         return;

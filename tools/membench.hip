@@ -319,6 +319,25 @@ __global__ __launch_bounds__(256) void k_policy(const uint8_t* __restrict__ src,
         reinterpret_cast<u32x4*>(dst)[threadIdx.x] = acc;
 }
 
+// Write-only row patterns of the fan-out kernel: each wave stores RW
+// consecutive 1 KiB rows (RW * 64 lanes... one 16-B chunk per lane per row)
+// per pass, passes strided by the whole grid; SC1 = write-through stores.
+template <int RW, bool SC1>
+__global__ __launch_bounds__(64 * RW) void k_rows(uint8_t* __restrict__ dst, uint64_t rows, uint32_t key)
+{
+    const uint64_t wave_rows = uint64_t(gridDim.x) * RW;
+    for (uint64_t r = uint64_t(blockIdx.x) * RW + threadIdx.x / 64; r < rows; r += wave_rows) {
+        const u32x4 w = u32x4{uint32_t(r), key, threadIdx.x, key};
+        uint8_t* row = dst + r * 1024;
+        if (SC1) {
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(row, 0, 1024, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(w, rs, (threadIdx.x & 63) * 16, 0, 16);
+        } else {
+            __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(row) + (threadIdx.x & 63));
+        }
+    }
+}
+
 template <class F>
 double time_kernel(F launch, int reps = 20)
 {
@@ -442,6 +461,23 @@ int main(int argc, char** argv)
         }
 #undef POL
         CK(hipFree(base));
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "wpattern") {
+        // the fan-out's output (41,040,000 B) written by row patterns: one
+        // 1 KiB row per wave per pass (the period kernel) vs 2 / 4 / 16
+        // consecutive rows per block, nontemporal vs write-through, over
+        // several wave counts; b2b = launches back to back
+        const uint64_t bytes41 = 41040000ull / 1024 * 1024;
+        uint8_t* d;
+        CK(hipMalloc(&d, 2 * bytes41 + 4096));
+        const uint64_t rows = bytes41 / 1024;
+#define WP(RW, SC1)                                                                                                 for (int wpc : {4, 8, 16, 32}) {                                                                                    const int blocks = std::max(1, cus * wpc / RW);                                                                 double ms = time_kernel([&](int i) { k_rows<RW, SC1><<<blocks, 64 * RW>>>(d + (i & 1) * bytes41, rows, 7u); });         printf("rows RW=%2d sc1=%d waves/CU=%2d  %8.2f us  %7.1f GB/s\n", RW, int(SC1), wpc, ms * 1e3,                            bytes41 / (ms * 1e-3) / 1e9);                                                                        }
+        for (int rep = 0; rep < 2; ++rep) {
+            WP(1, false) WP(1, true) WP(2, true) WP(4, false) WP(4, true) WP(16, true)
+        }
+#undef WP
+        CK(hipFree(d));
         return 0;
     }
     if (argc > 2 && std::string(argv[2]) == "grid") {
