@@ -51,7 +51,7 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #define WSG_DIAG 0   // 5: timing-only diagnostic build of k_decode (every tile streams; tools/)
 #endif
 #ifndef WSG_DIAG_FAN
-#define WSG_DIAG_FAN 0   // timing-only fan-out diagnostics: 1 no key loads, 2 no payload loads, 4 stores only, 8 no edge blocks; period path: 16 no template loads, 32 no key loads
+#define WSG_DIAG_FAN 0   // timing-only fan-out diagnostics: 1 no key loads, 2 no payload loads, 4 stores only, 8 no edge blocks; period path: 16 no template loads, 32 no key loads, 64 no stores
 #endif
 #ifndef WSG_DIAG_NOINFO
 #define WSG_DIAG_NOINFO 0   // timing-only: k_decode without its per-frame info slice (tools/)
@@ -1494,16 +1494,38 @@ __global__ __launch_bounds__(BLOCK) void k_fanout_flat(const uint8_t* __restrict
 // blockIdx.y picks message y of up to FAN_MSGS messages of one geometry
 // (length, opcode), whose payload and output start come from the kernel
 // arguments; the k frames of every message are written exactly as for one.
+// Template and key mask of frame bytes [o, o + 16) (o < fsize): t = the
+// bytes with a zero key (header with the key bytes 0, close status 0, raw
+// payload; 0 past the frame), m = the bytes the key is XORed into ([kpos,
+// fsize): mask key, status, payload), so the frame with key K is
+// t ^ (m & key_rot(K, o - hdr)).
+__device__ __forceinline__ void fan_tm(const uint8_t* __restrict__ payload, uint64_t len, const FanGeom& f,
+                                       uint64_t fsize, uint64_t o, v4u& t, v4u& m)
+{
+    const uint64_t hi = fsize - o < CHUNK ? fsize - o : CHUNK;
+    const uint64_t kl = o < f.kpos ? f.kpos - o : 0;
+    const uint64_t lo = o < f.data0 ? f.data0 - o : 0;   // chunk bytes [lo, hi) are payload
+    m = low_bytes(hi) & ~low_bytes(kl);
+    t = shr_bytes(f.hp0, o);
+    if (lo < hi)
+        t |= fan_window(payload, len, int64_t(o) - int64_t(f.data0)) & (low_bytes(hi) & ~low_bytes(lo));
+}
+
 template <int P>
 __global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict__ payload0, uint64_t len,
                                                       const uint32_t* __restrict__ keys, uint32_t k, uint8_t opcode,
                                                       uint32_t mask, uint64_t fsize, uint32_t G, uint32_t dm,
-                                                      uint8_t* __restrict__ wire0, const FanMsgs msgs)
+                                                      uint8_t* __restrict__ wire0, const FanMsgs msgs, v4u hp0)
 {
     constexpr int KW = 2 * P;   // keys per pass: the row spans <= 2 groups (G >= 64)
     const uint8_t* __restrict__ payload = payload0 + msgs.src[blockIdx.y];
     uint8_t* __restrict__ wire = wire0 + msgs.dst[blockIdx.y];
-    const FanGeom f = fan_geom(opcode, mask != 0, len);
+    FanGeom f;   // fan_geom() with the header bytes from the host (hp0)
+    f.g = send_geom(opcode, mask != 0, len, 0);
+    f.data0 = f.g.hdr + f.g.prefix;
+    f.kpos = f.g.hdr - (mask ? 4u : 0u);
+    f.mask = mask != 0;
+    f.hp0 = hp0;
     const uint64_t total = fsize * k;
     const uint64_t chunks = (total + CHUNK - 1) / CHUNK;
     const uint32_t lane = threadIdx.x & 63;
@@ -1514,58 +1536,84 @@ __global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict_
     const uint64_t rstep = uint64_t(gridDim.x) * wpb * 64;   // W rows: a multiple of G (dm groups)
     if (row0 >= chunks)
         return;
-    const uint64_t m0 = row0 / G;                        // first group of pass 0
+    const uint64_t m0 = (row0 >> 32) ? row0 / G : uint64_t(uint32_t(row0) / G);   // first group of pass 0
     const uint32_t jw = uint32_t(row0 - m0 * G);         // group position of lane 0
     const uint32_t dl = (jw + lane) >= G ? 1u : 0u;      // lane's group: m0 + dl (+ it * dm)
     const uint32_t j = jw + lane - dl * G;
 
-    // template of chunk j
-    const uint64_t o = uint64_t(j) * CHUNK;
-    const uint32_t qa = uint32_t(o / fsize);             // frame of the group holding byte o
+    // template of chunk j: its frame-a bytes, and the next frame's from byte
+    // `split` on (the first 16 bytes of a frame: the same for every lane)
+    const uint64_t o = uint64_t(j) * CHUNK;              // < P * fsize
+    uint32_t qa = 0;                                     // frame of the group holding byte o
+#pragma unroll
+    for (int q = 1; q < P; ++q)
+        qa += o >= uint64_t(q) * fsize ? 1u : 0u;
     const uint64_t r = o - uint64_t(qa) * fsize;
-    const v4u ta = (WSG_DIAG_FAN & 16) ? v4u{j, 1, 2, 3} : fan_frame_bytes(payload, len, f, fsize, 0u, r);
-    const v4u ma = (WSG_DIAG_FAN & 16) ? v4u{~0u, ~0u, ~0u, ~0u} : ta ^ fan_frame_bytes(payload, len, f, fsize, ~0u, r);
+    v4u t, ma, mb = {0, 0, 0, 0};
+    if (WSG_DIAG_FAN & 16) {
+        t = v4u{j, 1, 2, 3};
+        ma = v4u{~0u, ~0u, ~0u, ~0u};
+    } else {
+        fan_tm(payload, len, f, fsize, r, t, ma);
+    }
     const uint64_t split = fsize - r;                    // the next frame starts at chunk byte `split`
-    v4u t = ta, mb = {0, 0, 0, 0};
     if (split < CHUNK) {
-        const v4u tb = fan_frame_bytes(payload, len, f, fsize, 0u, 0);
-        t ^= shl_bytes(tb, split);
-        mb = shl_bytes(tb ^ fan_frame_bytes(payload, len, f, fsize, ~0u, 0), split);
+        v4u t0, m0v;
+        fan_tm(payload, len, f, fsize, 0, t0, m0v);
+        t |= shl_bytes(t0, split);
+        mb = shl_bytes(m0v, split);
     }
     const uint32_t pa = uint32_t(r - f.g.hdr), pb = uint32_t(0u - uint32_t(split) - f.g.hdr);
     const uint32_t ia = P * dl + qa;                     // key slots of this pass's window
 
     // keys of every pass: slot it * KW + q -> key P * (m0 + it * dm) + q
-    const uint64_t passes = (chunks - row0 + rstep - 1) / rstep;   // host: passes * KW <= 64 * WSG_FAN_KV
+    // (host: passes * KW <= 64 * WSG_FAN_KV)
     uint32_t kv[WSG_FAN_KV];
 #pragma unroll
     for (int h = 0; h < WSG_FAN_KV; ++h) {
         const uint32_t s = uint32_t(h) * 64 + lane;
         const uint64_t it = s / KW;
         const uint64_t idx = uint64_t(P) * (m0 + it * dm) + (s % KW);
-        kv[h] = (WSG_DIAG_FAN & 32) ? uint32_t(idx) : (it < passes && idx < k) ? keys[idx] : 0u;
+        kv[h] = (WSG_DIAG_FAN & 32) ? uint32_t(idx) : (row0 + it * rstep < chunks && idx < k) ? keys[idx] : 0u;
     }
 
-    for (uint32_t it = 0; it < passes; ++it) {
-        const uint64_t c = row0 + uint64_t(it) * rstep + lane;
-        const uint32_t slot = it * KW;                           // wave-uniform; KW divides 64
+    // Pass loop, kept lean (it is most of the kernel's instructions): running
+    // row / pointer / shuffle-address registers instead of per-pass products,
+    // rotations as one v_alignbit each, and a wave-uniform test for whole
+    // rows, so a pass is ~2 shuffles, ~12 VALU and one 1 KiB store.
+    const uint32_t sa = 8u * (pa & 3u), sbr = 8u * (pb & 3u);
+    const uint64_t full_rows_end = chunks & ~uint64_t(63);   // rows below this are whole (64 chunks)
+    uint64_t row = row0;
+    uint8_t* wrow = wire + row0 * CHUNK;
+    const uint64_t wstep = rstep * CHUNK;
+    uint32_t addr = ia * 4;                                 // shuffle address of key slot ia of pass 0
+#pragma unroll 1
+    for (uint32_t it = 0; row < chunks; ++it) {
+        const uint32_t slot = it * KW;                      // wave-uniform; KW divides 64
         uint32_t kreg = kv[0];
 #pragma unroll
         for (int h = 1; h < WSG_FAN_KV; ++h)
             kreg = (slot >> 6) == uint32_t(h) ? kv[h] : kreg;
         const uint32_t sb = (slot & 63) * 4;
-        const uint32_t ka = __builtin_amdgcn_ds_bpermute(int(sb + ia * 4), int(kreg));
-        const uint32_t kb = __builtin_amdgcn_ds_bpermute(int(sb + (ia + 1) * 4), int(kreg));
-        const uint32_t ra = key_rot(ka, pa), rb = key_rot(kb, pb);
+        const uint32_t ka = __builtin_amdgcn_ds_bpermute(int(addr + sb), int(kreg));
+        const uint32_t kb = __builtin_amdgcn_ds_bpermute(int(addr + sb + 4), int(kreg));
+        const uint32_t ra = __builtin_amdgcn_alignbit(ka, ka, sa), rb = __builtin_amdgcn_alignbit(kb, kb, sbr);
         const v4u w = t ^ (ma & v4u{ra, ra, ra, ra}) ^ (mb & v4u{rb, rb, rb, rb});
-        if (WSG_FAN_SC1 && c + 1 < chunks) {
-            // write-through store of a whole chunk (resource at the pass row)
-            const uint64_t row = row0 + uint64_t(it) * rstep;
-            const OutTile ot(wire + row * CHUNK, 64 * CHUNK, true);
-            ot.put(lane * CHUNK, w);
-        } else if (c < chunks) {
-            fan_store(wire, c, chunks, total, w);
+        if ((WSG_DIAG_FAN & 64) && (w[0] & w[1] & w[2] & w[3]) != 0xA5C3E1F7u) {
+            // diagnostic: the computation without its stores
+        } else if (row < full_rows_end) {
+            // a whole row: one 16-B store per lane
+            if (WSG_FAN_SC1) {
+                const OutTile ot(wrow, 64 * CHUNK, true);   // write-through (resource at the row)
+                ot.put(lane * CHUNK, w);
+            } else {
+                st16nt(wrow + lane * CHUNK, w);
+            }
+        } else if (row + lane < chunks) {
+            fan_store(wire, row + lane, chunks, total, w);   // the last, partial row
         }
+        row += rstep;
+        wrow += wstep;
     }
 }
 
@@ -1705,15 +1753,22 @@ bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_
         return false;
     const uint32_t dm = uint32_t(W * 64 / G);
     const uint64_t wpb = 1;   // waves per block: one (4-wave blocks measured 8 % slower at C4)
+    // header bytes before the key (<= 10), the same in every frame
+    const SendGeom sg = send_geom(opcode, mask != 0, len, 0);
+    const uint32_t kpos = sg.hdr - (mask ? 4u : 0u);
+    uint32_t hw[4] = {0, 0, 0, 0};
+    for (uint32_t r = 0; r < kpos; ++r)
+        hw[r / 4] |= uint32_t(header_byte(opcode, mask != 0, sg.body, 0, r)) << (8 * (r % 4));
+    const v4u hp0 = v4u{hw[0], hw[1], hw[2], hw[3]};
     switch (P) {
     case 1:
-        k_fanout_period<1><<<dim3(uint32_t(W / wpb), nmsgs), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire, msgs);
+        k_fanout_period<1><<<dim3(uint32_t(W / wpb), nmsgs), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire, msgs, hp0);
         break;
     case 2:
-        k_fanout_period<2><<<dim3(uint32_t(W / wpb), nmsgs), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire, msgs);
+        k_fanout_period<2><<<dim3(uint32_t(W / wpb), nmsgs), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire, msgs, hp0);
         break;
     default:
-        k_fanout_period<4><<<dim3(uint32_t(W / wpb), nmsgs), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire, msgs);
+        k_fanout_period<4><<<dim3(uint32_t(W / wpb), nmsgs), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire, msgs, hp0);
         break;
     }
     *err = hipGetLastError();

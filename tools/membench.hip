@@ -322,6 +322,13 @@ __global__ __launch_bounds__(256) void k_policy(const uint8_t* __restrict__ src,
 // Write-only row patterns of the fan-out kernel: each wave stores RW
 // consecutive 1 KiB rows (RW * 64 lanes... one 16-B chunk per lane per row)
 // per pass, passes strided by the whole grid; SC1 = write-through stores.
+// an (almost) empty kernel: the launch / wave start-up floor of a grid
+__global__ void k_empty(uint32_t* out, uint32_t v)
+{
+    if (v == 0xFFFFFFFFu)
+        out[threadIdx.x] = v;
+}
+
 template <int RW, bool SC1>
 __global__ __launch_bounds__(64 * RW) void k_rows(uint8_t* __restrict__ dst, uint64_t rows, uint32_t key)
 {
@@ -461,6 +468,19 @@ int main(int argc, char** argv)
         }
 #undef POL
         CK(hipFree(base));
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "empty") {
+        // launch floor: back-to-back empty kernels of 64-thread and 256-thread blocks
+        uint32_t* d;
+        CK(hipMalloc(&d, 4096));
+        for (int rep = 0; rep < 2; ++rep)
+            for (int blocks : {256, 1024, 2048, 4096, 8192})
+                for (int threads : {64, 256}) {
+                    double ms = time_kernel([&](int) { k_empty<<<blocks, threads>>>(d, 1u); });
+                    printf("empty blocks=%5d threads=%3d %8.2f us\n", blocks, threads, ms * 1e3);
+                }
+        CK(hipFree(d));
         return 0;
     }
     if (argc > 2 && std::string(argv[2]) == "wpattern") {
