@@ -508,6 +508,25 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
     if (!WSG_DEC_INFO_LAST)
         info_slice();
 
+#if WSG_DIAG == 6   // timing-only: the launch as a bare copy-with-XOR of the full tiles (no frame logic)
+    for (uint64_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
+        const uint64_t base = t * TILE;
+        if (base + TILE > wire_len)
+            break;
+        v4u v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            v[u] = ld16nt(wire + base + lane_off(u));
+#ifdef WSG_DIAG_ORD
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+            st16nt(out + base + lane_off(u), v[u] ^ 0x9u);
+    }
+    return;
+#endif
     for (uint64_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
         const uint64_t base = t * TILE;
         const uint64_t tend = min(base + TILE, wire_len);
@@ -517,7 +536,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
         // coarse probe of the frame table (vector load, issued before the
         // data loads: loads return in issue order)
         const uint64_t g = tile_guess(n, frames_per_byte, base);
+#if WSG_DIAG == 7   // timing-only: no coarse probe (right only where the guess is exact: equal-size frames)
+        const uint64_t probe = 0;
+#else
         const uint64_t probe = fs[probe_index(g, stride, n, int(threadIdx.x & 63))];
+#endif
         __builtin_amdgcn_sched_barrier(0);
 
         // the tile's data does not depend on frame metadata: issue it next

@@ -345,6 +345,114 @@ __global__ __launch_bounds__(64 * RW) void k_rows(uint8_t* __restrict__ dst, uin
     }
 }
 
+// LDS-DMA streaming copy-with-XOR: each wave owns pieces of U KiB (dealt
+// round-robin over all waves of a resident grid) and loads them with
+// global_load_lds_dwordx4 into a D-deep per-wave ring in LDS, so D-1 pieces
+// stay in flight without holding VGPRs; ds_read_b128 -> XOR -> store.  vmcnt
+// counts loads and stores in issue order, so the wait for piece q's DMA
+// leaves exactly the ops issued after it outstanding (counted at run time).
+// SP: 0 plain, 1 nontemporal, 2 write-through (sc1 buffer) stores.
+__device__ __forceinline__ void wait_vm_le(int n)
+{
+    // s_waitcnt vmcnt(n) for n in multiples of 4 up to 60 (larger: 60 waits more: safe)
+    switch (n >> 2) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
+    }
+}
+
+template <int WPB, int D, int U, int SP>
+__global__ __launch_bounds__(64 * WPB) void k_glds(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   uint64_t pieces, uint32_t key)
+{
+    __shared__ u32x4 ring[WPB * D * U * 64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t waves = uint64_t(gridDim.x) * WPB;
+    const uint64_t q0 = uint64_t(blockIdx.x) * WPB + w;
+    constexpr uint64_t PB = uint64_t(U) * 1024;
+    u32x4* my = ring + w * (D * U * 64);
+    auto issue = [&](uint64_t q, int slot) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(src + q * PB + u * 1024 + lane * 16),
+                (__attribute__((address_space(3))) void*)(my + (slot * U + u) * 64), 16, 0, 2);
+    };
+    int issued = 0;   // pieces issued ahead of the one being consumed
+#pragma unroll
+    for (int i = 0; i < D - 1; ++i)
+        if (q0 + uint64_t(i) * waves < pieces) {
+            issue(q0 + uint64_t(i) * waves, i);
+            ++issued;
+        }
+    int stores_after = 0;   // stores issued after the oldest outstanding piece's loads
+    int slot = 0;
+    for (uint64_t q = q0; q < pieces; q += waves) {
+        const uint64_t qn = q + uint64_t(D - 1) * waves;
+        int loads_after = (issued - 1) * U;   // loads issued after piece q's
+        if (qn < pieces) {
+            issue(qn, (slot + D - 1) % D);
+            loads_after += U;
+        } else {
+            --issued;
+        }
+        wait_vm_le(loads_after + stores_after);
+        // ds_read in inline asm: hipcc otherwise waits vmcnt(0) before any
+        // LDS read while a DMA is in flight (it cannot tell the ring slots
+        // apart); the lgkmcnt wait takes the values as operands so nothing
+        // uses them before it
+        const uint32_t la = uint32_t(reinterpret_cast<uintptr_t>(
+                                (__attribute__((address_space(3))) u32x4*)(my + slot * U * 64 + lane)));
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v[u]) : "v"(la), "i"(u * 1024));
+        if (U == 2)
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[U > 1 ? 1 : 0]));
+        else if (U == 4)
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[U > 2 ? 2 : 0]), "+v"(v[U > 3 ? 3 : 0]));
+        else {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                asm volatile("" : "+v"(v[u]));
+        }
+        if (SP == 2) {
+            const auto rd = __builtin_amdgcn_make_buffer_rsrc(dst + q * PB, 0, uint32_t(PB), 0x00020000);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                __builtin_amdgcn_raw_buffer_store_b128(v[u] ^ key, rd, (u * 64 + lane) * 16, 0, 16);
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                u32x4* o = reinterpret_cast<u32x4*>(dst + q * PB) + u * 64 + lane;
+                if (SP == 1)
+                    __builtin_nontemporal_store(v[u] ^ key, o);
+                else
+                    *o = v[u] ^ key;
+            }
+        }
+        // after the next piece's loads come these stores; older stores are
+        // retired by the next wait with the loads they precede
+        stores_after = min(stores_after + U, (D - 1) * U);
+        slot = (slot + 1) % D;
+    }
+}
+
 template <class F>
 double time_kernel(F launch, int reps = 20)
 {
@@ -498,6 +606,106 @@ int main(int argc, char** argv)
         }
 #undef WP
         CK(hipFree(d));
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "data") {
+        // does the copy's rate depend on the bytes? the 16 KiB-tile copy at
+        // 48 blocks/CU over two pairs, sources of constant bytes vs random
+        // bytes (splitmix64), interleaved
+        const uint64_t span = 4 * bytes;
+        uint8_t* base;
+        CK(hipMalloc(&base, span));
+        std::vector<uint64_t> h(bytes / 8);
+        uint64_t x = 12345;
+        for (auto& w : h) {
+            uint64_t z = (x += 0x9e3779b97f4a7c15ull);
+            z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+            z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+            w = z ^ (z >> 31);
+        }
+        auto P = [&](uint64_t off) { return (u32x4*)(base + off); };
+        const int grid = cus * 48;
+        auto launch = [&](int i) {
+            const uint64_t s = (i & 1) * 2 * bytes;
+            k_stream<256, 4, 3><<<grid, 256>>>(P(s), P(s + bytes), n16, 9u);
+        };
+        for (int rep = 0; rep < 3; ++rep) {
+            for (int kind = 0; kind < 3; ++kind) {
+                // 0: constant 0x05, 1: zero, 2: random (both pairs' sources)
+                for (int pr = 0; pr < 2; ++pr) {
+                    if (kind == 2)
+                        CK(hipMemcpy(base + pr * 2 * bytes, h.data(), bytes, hipMemcpyHostToDevice));
+                    else
+                        CK(hipMemset(base + pr * 2 * bytes, kind == 0 ? 5 : 0, bytes));
+                }
+                CK(hipDeviceSynchronize());
+                const double ms = time_kernel(launch);
+                printf("copy 16K tiles bpc=48 src=%-8s %8.1f us %7.1f GB/s\n",
+                       kind == 0 ? "const05" : kind == 1 ? "zero" : "random", ms * 1e3,
+                       2.0 * bytes / (ms * 1e-3) / 1e9);
+            }
+        }
+        CK(hipFree(base));
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "glds") {
+        // LDS-DMA pipelined copy (k_glds) against the register copy at the
+        // C2 footprint, two source/destination pairs in turn; resident grids.
+        // After each timing, one launch on a cleared destination is checked
+        // word for word (src ^ key).
+        const uint64_t span = 4 * bytes;
+        uint8_t* base;
+        CK(hipMalloc(&base, span));
+        CK(hipMemset(base, 5, span));
+        {
+            std::vector<uint32_t> h(bytes / 4);
+            for (size_t k = 0; k < h.size(); ++k)
+                h[k] = uint32_t(k * 2654435761u);
+            CK(hipMemcpy(base, h.data(), bytes, hipMemcpyHostToDevice));
+        }
+        std::vector<uint32_t> hs(bytes / 4), hd(bytes / 4);
+        CK(hipMemcpy(hs.data(), base, bytes, hipMemcpyDeviceToHost));
+        auto P = [&](uint64_t off) { return (u32x4*)(base + off); };
+        auto report = [&](const char* name, int grid, double ms, auto launch) {
+            CK(hipMemset(base + bytes, 0, bytes));
+            launch(0);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(hd.data(), base + bytes, bytes, hipMemcpyDeviceToHost));
+            size_t bad = 0;
+            for (size_t k = 0; k < hs.size(); ++k)
+                bad += hd[k] != (hs[k] ^ 9u);
+            printf("%-40s grid=%6d %8.1f us %7.1f GB/s%s\n", name, grid, ms * 1e3, 2.0 * bytes / (ms * 1e-3) / 1e9,
+                   bad ? "  MISMATCH" : "");
+        };
+#define GL(WPB, D, U, SP, BPC)                                                                                 \
+    {                                                                                                          \
+        const uint64_t pieces = bytes / (U * 1024);                                                            \
+        const int grid = cus * BPC;                                                                            \
+        auto launch = [&](int i) {                                                                             \
+            const uint64_t s = (i & 1) * 2 * bytes;                                                            \
+            k_glds<WPB, D, U, SP><<<grid, 64 * WPB>>>(base + s, base + s + bytes, pieces, 9u);                 \
+        };                                                                                                     \
+        report("glds wpb=" #WPB " D=" #D " U=" #U " sp=" #SP " bpc=" #BPC, grid, time_kernel(launch), launch);  \
+    }
+        for (int rep = 0; rep < 2; ++rep) {
+            {
+                const int grid = cus * 48;
+                auto launch = [&](int i) {
+                    const uint64_t s = (i & 1) * 2 * bytes;
+                    k_stream<256, 4, 3><<<grid, 256>>>(P(s), P(s + bytes), n16, 9u);
+                };
+                report("register copy 16K tiles nt/nt bpc=48", grid, time_kernel(launch), launch);
+            }
+            GL(4, 2, 4, 1, 5) GL(4, 2, 4, 2, 5) GL(4, 2, 4, 0, 5)
+            GL(4, 3, 4, 1, 3) GL(4, 3, 4, 2, 3)
+            GL(2, 4, 4, 1, 4) GL(2, 4, 4, 2, 4)
+            GL(4, 2, 8, 1, 2) GL(4, 2, 8, 2, 2)
+            GL(2, 3, 8, 1, 3) GL(2, 3, 8, 2, 3)
+            GL(4, 2, 2, 1, 8) GL(4, 2, 2, 2, 8)
+            GL(1, 4, 4, 1, 8) GL(1, 4, 4, 2, 8)
+        }
+#undef GL
+        CK(hipFree(base));
         return 0;
     }
     if (argc > 2 && std::string(argv[2]) == "grid") {

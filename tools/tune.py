@@ -42,6 +42,16 @@ def main():
                                                for r in range(rot - 1)]
         f = torch.from_numpy(fs.view(np.int64)).cuda()
     outs = [torch.empty_like(ws[0]) for _ in range(rot)]
+    if os.environ.get("ARENA") == "1":
+        # every wire and output carved from ONE allocation (16 KiB-aligned
+        # slots), as a server's preallocated batch arena would hold them
+        slot = (ws[0].numel() + 16383) // 16384 * 16384
+        arena = torch.empty(2 * rot * slot, dtype=torch.uint8, device="cuda")
+        for r in range(rot):
+            a = arena[2 * r * slot: 2 * r * slot + ws[0].numel()]
+            a.copy_(ws[r])
+            ws[r] = a
+            outs[r] = arena[(2 * r + 1) * slot: (2 * r + 1) * slot + ws[0].numel()]
     info = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
     it = [0]
 
