@@ -27,7 +27,7 @@ struct wsg_ctx {
     int num_cus = 256;
     int blocks_per_cu = 32;       // encode / fan-out / xor grids
     int enc_blocks_per_cu = 1024; // k_encode_mask grid, ~1-2 pieces per wave (tools/tune_enc.py: C5 share -15 %, C3-like -6 % vs 32)
-    int dec_blocks_per_cu = 48;   // k_decode grid: 40-56 best, 48 chosen (tools/tune.py: C2 -3.5 %, C3 ragged -2 % vs 32)
+    int dec_blocks_per_cu = 256;  // k_decode grid (tools/tune.py, round 2): C2 best from 64 up (one tile per block, -1 % vs 48); C3 ragged 256 (two tiles per block: -9.7 % vs 48; 128: -5.6 %, 320-512: -5.8 %, 1024: 0)
     int fan_waves_per_cu = 8;    // fan-out period path: waves per CU (tools/tune_enc.py CFG=c4: 8 best of 4-32)
     uint64_t small_avg = wsg::SMALL_AVG;   // batch encode: k_encode_small when wire_cap <= n * small_avg
     unsigned long long* d_err = nullptr;        // latch of the caller-visible async entry points (wsg_sync)

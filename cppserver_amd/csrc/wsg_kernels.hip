@@ -408,7 +408,6 @@ __device__ __forceinline__ uint32_t probe_index(uint64_t g, uint32_t stride, uin
 __device__ __forceinline__ void locate(const uint64_t* __restrict__ fs, uint32_t n, uint64_t g, uint32_t stride,
                                        uint64_t probe, uint64_t base, TileLoc& L)
 {
-    const uint64_t below = __ballot(probe <= base);   // a prefix of the lanes for a sorted table
     uint64_t w[MAXF + 2];
 #pragma unroll
     for (int k = 0; k < MAXF + 2; ++k) {
@@ -423,7 +422,9 @@ __device__ __forceinline__ void locate(const uint64_t* __restrict__ fs, uint32_t
             L.st[k] = w[k];
         return;
     }
-    // candidates [a, b) for the last start <= base, fs[a - 1] <= base < fs[b]
+    // candidates [a, b) for the last start <= base, fs[a - 1] <= base < fs[b];
+    // the probe is consulted only here, so a hit of the guess never waits for it
+    const uint64_t below = __ballot(probe <= base);   // a prefix of the lanes for a sorted table
     const int m = __builtin_popcountll(below);
     uint32_t a = m > 0 ? probe_index(g, stride, n, m - 1) + 1 : 0;
     uint32_t b = m < 64 ? probe_index(g, stride, n, m) : n;
@@ -537,26 +538,35 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
         // data loads: loads return in issue order)
         const uint64_t g = tile_guess(n, frames_per_byte, base);
 #if WSG_DIAG == 7   // timing-only: no coarse probe (right only where the guess is exact: equal-size frames)
-        const uint64_t probe = 0;
+        uint64_t probe = 0;
 #else
         const uint64_t probe = fs[probe_index(g, stride, n, int(threadIdx.x & 63))];
 #endif
+        // Only a guess miss reads the probe.  Used on that path alone, the
+        // load would be sunk into it, behind the data loads (vector loads
+        // return in issue order: a ragged tile would wait for its data
+        // before searching), so every path ends with keep_probe(): a test
+        // that is never true for a batch the host launches (n > 0), after
+        // the tile's stores, where the probe is long back.
+        auto keep_probe = [&]() {
+            if (n == 0 && probe == ~uint64_t(0))
+                out[0] = 0;
+        };
         __builtin_amdgcn_sched_barrier(0);
 
-        // the tile's data does not depend on frame metadata: issue it next
-        // (the wire's last tile reads whole 16-B blocks up to its end)
+        // the tile's data does not depend on frame metadata: issue it next,
+        // unconditionally, so that the metadata chain below waits for the
+        // probe alone (vmcnt(UNROLL)); loads behind a branch made the compiler
+        // wait vmcnt(0) there, i.e. start the chain only once the whole tile
+        // had arrived.  The wire's last, partial tile takes the staged path,
+        // which reads its bytes itself: its loads here are clamped to the
+        // 16-B block holding the last wire byte (readable by contract) and
+        // their values are not used.
+        const uint64_t last_blk = (wire_len - 1) & ~uint64_t(CHUNK - 1);
         v4u v[UNROLL];
-        if (full) {
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
-                v[u] = ld16nt(wire + base + lane_off(u));
-        } else {
-            // the wire's last, partial tile always takes the staged path,
-            // which reads its bytes itself (never past the wire's end)
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
-                v[u] = v4u{0, 0, 0, 0};
-        }
+        for (int u = 0; u < UNROLL; ++u)
+            v[u] = ld16nt(wire + min(base + lane_off(u), last_blk));
 
         TileLoc L;
         locate(fs, n, g, stride, probe, base, L);
@@ -594,6 +604,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
 #pragma unroll
                 for (int u = 0; u < UNROLL; ++u)
                     ot.put(uint32_t(lane_off(u)), v[u] ^ S[0].kr);
+                keep_probe();
                 continue;
             }
             const OutTile ot(out + base, uint32_t(TILE));
@@ -618,6 +629,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
                 }
                 ot.put(o, v[u] ^ x);
             }
+            keep_probe();
             continue;
         }
 
@@ -732,6 +744,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
                 }
             }
         }
+        keep_probe();
     }
     if (WSG_DEC_INFO_LAST)
         info_slice();
