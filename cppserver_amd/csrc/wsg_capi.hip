@@ -27,7 +27,8 @@ struct wsg_ctx {
     int num_cus = 256;
     int blocks_per_cu = 32;       // encode / fan-out / xor grids
     int enc_blocks_per_cu = 1024; // k_encode_mask grid, ~1-2 pieces per wave (tools/tune_enc.py: C5 share -15 %, C3-like -6 % vs 32)
-    int dec_blocks_per_cu = 256;  // k_decode grid (tools/tune.py, round 2): C2 best from 64 up (one tile per block, -1 % vs 48); C3 ragged 256 (two tiles per block: -9.7 % vs 48; 128: -5.6 %, 320-512: -5.8 %, 1024: 0)
+    int dec_tiles_per_block = 0;   // 0: grid from dec_blocks_per_cu alone; k: ceil(tiles / k) blocks (A/B)
+    int dec_blocks_per_cu = 4096;  // k_decode grid cap: one 16 KiB tile per block up to 16 GiB of wire (tools/tune.py, round 2: C2 84.3 vs 85.1 us at 48 blocks/CU, 88.1 at two tiles per block; C3 ragged 0.685 vs 0.705 ms at 256, 0.783 at 48)
     int fan_waves_per_cu = 8;    // fan-out period path: waves per CU (tools/tune_enc.py CFG=c4: 8 best of 4-32)
     uint64_t small_avg = wsg::SMALL_AVG;   // batch encode: k_encode_small when wire_cap <= n * small_avg
     unsigned long long* d_err = nullptr;        // latch of the caller-visible async entry points (wsg_sync)
@@ -264,8 +265,13 @@ int wsg_create(int device, wsg_ctx** out)
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (const char* e = std::getenv("WSG_BLOCKS_PER_CU")) {
         const int v = std::atoi(e);
-        if (v > 0 && v <= 256)
+        if (v > 0 && v <= 4096)
             c->blocks_per_cu = c->dec_blocks_per_cu = c->enc_blocks_per_cu = v;   // A/B runs: every grid
+    }
+    if (const char* e = std::getenv("WSG_DEC_TILES_PER_BLOCK")) {   // A/B measurements (tools/tune.py)
+        const int v = std::atoi(e);
+        if (v >= 0 && v <= 64)
+            c->dec_tiles_per_block = v;
     }
     if (const char* e = std::getenv("WSG_ENC_BLOCKS_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
         const int v = std::atoi(e);
@@ -379,7 +385,8 @@ int decode_launch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const ui
     // a short (or empty) wire are still checked
     const uint64_t tiles = ceil_div(wire_len, wsg::TILE);
     const int t = timing_begin(c, s);
-    WSG_HIP(wsg::launch_decode(s, grid_for(c, std::max(tiles, ceil_div(n, wsg::BLOCK)), c->dec_blocks_per_cu), d_wire, d_out, wire_len,
+    const uint64_t units = c->dec_tiles_per_block ? ceil_div(tiles, uint64_t(c->dec_tiles_per_block)) : tiles;
+    WSG_HIP(wsg::launch_decode(s, grid_for(c, std::max(units, ceil_div(n, wsg::BLOCK)), c->dec_blocks_per_cu), d_wire, d_out, wire_len,
                                d_frame_start, n, d_info, err));
     timing_end(c, s, t);
     return WSG_OK;

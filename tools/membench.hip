@@ -112,6 +112,23 @@ __global__ __launch_bounds__(256) void k_map(const u32x4* __restrict__ src, u32x
     }
 }
 
+// One 16 KiB tile per block; which tile block b takes: W-way interleave of
+// W equal regions (W = 1: linear), i.e. W address streams advance together
+template <int W>
+__global__ __launch_bounds__(256) void k_ways(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t tiles,
+                                              uint32_t key)
+{
+    const uint64_t per = tiles / W;
+    const uint64_t t = (blockIdx.x % W) * per + blockIdx.x / W;
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        v[u] = __builtin_nontemporal_load(src + t * 1024 + uint64_t(u) * 256 + threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        __builtin_nontemporal_store(v[u] ^ key, dst + t * 1024 + uint64_t(u) * 256 + threadIdx.x);
+}
+
 template <int MAP>
 void run_map(const char* name, u32x4* const* srcs, u32x4* const* dsts, uint64_t n16, int grid)
 {
@@ -606,6 +623,38 @@ int main(int argc, char** argv)
         }
 #undef WP
         CK(hipFree(d));
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "ways") {
+        // address streams: one tile per block, W-way interleaved regions,
+        // against grid-stride loops of 1, 2 and 4 tiles per block; two pairs
+        const uint64_t span = 4 * bytes;
+        uint8_t* base;
+        CK(hipMalloc(&base, span));
+        CK(hipMemset(base, 5, span));
+        auto P = [&](uint64_t off) { return (u32x4*)(base + off); };
+        const uint64_t tiles = n16 / 1024;
+        auto show = [&](const char* name, double ms) {
+            printf("%-36s %8.1f us %7.1f GB/s\n", name, ms * 1e3, 2.0 * tiles * 16384 / (ms * 1e-3) / 1e9);
+        };
+#define WAYS(W)                                                                                                \
+    show("one tile per block, " #W "-way", time_kernel([&](int i) {                                            \
+             const uint64_t s = (i & 1) * 2 * bytes;                                                           \
+             k_ways<W><<<int(tiles / W * W), 256>>>(P(s), P(s + bytes), tiles, 9u);                            \
+         }));
+        for (int rep = 0; rep < 2; ++rep) {
+            WAYS(1) WAYS(2) WAYS(4) WAYS(8) WAYS(16)
+            for (int per : {1, 2, 4}) {
+                char name[64];
+                snprintf(name, sizeof name, "grid-stride, %d tiles per block", per);
+                show(name, time_kernel([&](int i) {
+                         const uint64_t s = (i & 1) * 2 * bytes;
+                         k_stream<256, 4, 3><<<int(tiles / per), 256>>>(P(s), P(s + bytes), n16, 9u);
+                     }));
+            }
+        }
+#undef WAYS
+        CK(hipFree(base));
         return 0;
     }
     if (argc > 2 && std::string(argv[2]) == "data") {

@@ -1,6 +1,7 @@
 """Interleaved A/B timing of decode variants on the GPU box (medians).
 
-usage: python tools/tune.py [bpc ...]    (env WSG_BLOCKS_PER_CU per context)
+usage: python tools/tune.py [bpc[:tiles_per_block][@lib.so] ...]
+(env WSG_BLOCKS_PER_CU / WSG_DEC_TILES_PER_BLOCK per context)
 Each context is created with its own WSG_BLOCKS_PER_CU; runs are interleaved
 so clock/thermal drift hits every setting alike (guide §5.4 rule 24).
 """
@@ -61,8 +62,11 @@ def main():
         c.decode_batch(ws[k], f, out=outs[k], info=info)
     codecs = {}
     for b in settings:
-        bpc, _, path = b.partition("@")
+        # "BPC[:TPB][@lib]": blocks per CU cap, and tiles per block (0: off)
+        grid, _, path = b.partition("@")
+        bpc, _, tpb = grid.partition(":")
         os.environ["WSG_BLOCKS_PER_CU"] = bpc
+        os.environ["WSG_DEC_TILES_PER_BLOCK"] = tpb or "0"
         codecs[b] = ca.Codec(0, lib_path=path or None)
     every = int(os.environ.get("EVERY", 1))
     kern = {b: [] for b in settings}
