@@ -841,17 +841,18 @@ __device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirs
 // No load sits between two stores, so nothing here is a latency chain.
 __device__ __forceinline__ void edge_chunk(const FrameRec& R, uint64_t p, uint8_t* __restrict__ wire)
 {
-    const uintptr_t sbase = reinterpret_cast<uintptr_t>(R.src) - R.data_w;   // source of wire byte q: sbase + q
-    const uintptr_t src_lo = reinterpret_cast<uintptr_t>(R.src);
-    const uintptr_t src_hi = src_lo + (R.end - R.data_w);
-    const uintptr_t a = sbase + p;
-    const uint32_t s = uint32_t(a & 15u);
-    const uintptr_t a0 = a - s;
+    // source of wire byte q: R.src + (q - R.data_w); offsets from R.src
+    // (pointer arithmetic on the payload argument keeps the loads global_*:
+    // through uintptr_t they became flat loads, which count on lgkmcnt too)
+    const int64_t rel = int64_t(p - R.data_w);   // source offset of wire byte p
+    const uint32_t s = uint32_t((reinterpret_cast<uintptr_t>(R.src) + uint64_t(rel)) & 15u);
+    const int64_t r0 = rel - int64_t(s);           // aligned block holding it, relative to R.src
+    const int64_t data_len = int64_t(R.end - R.data_w);
     v4u lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
-    if (a0 < src_hi && a0 + 16 > src_lo)
-        lo = ld16(reinterpret_cast<const uint8_t*>(a0));
-    if (s != 0 && a0 + 16 < src_hi && a0 + 32 > src_lo)
-        hi = ld16(reinterpret_cast<const uint8_t*>(a0 + 16));
+    if (r0 < data_len && r0 + 16 > 0)
+        lo = ld16(R.src + r0);
+    if (s != 0 && r0 + 16 < data_len && r0 + 32 > 0)
+        hi = ld16(R.src + r0 + 16);
     const v4u d = s ? funnel(lo, hi, s) : lo;   // byte j: source byte of wire byte p + j
     v4u w = {0, 0, 0, 0};
     uint32_t own = 0;
@@ -891,7 +892,6 @@ template <bool NT>
 struct Piece {
     FrameRec R;
     uint64_t lo = 0, hi = 0;
-    uintptr_t sbase = 0;   // source of wire byte q: sbase + q
     uint32_t s = 0;        // source misalignment, uniform over the piece
     uint32_t kw = 0;       // key rotated to the piece's phase (uniform)
     bool live = false;
@@ -905,21 +905,25 @@ struct Piece {
         lo = (R.off & ~(PIECE_ALIGN - 1)) + k * PIECE;
         live = exists && lo < R.end;   // piece counts are an upper bound
         hi = min(lo + PIECE, R.end);
-        sbase = reinterpret_cast<uintptr_t>(R.src) - R.data_w;
-        s = (WSG_DIAG_ENC & 2) ? 0u : uint32_t((sbase + lo) & 15u);
+        // source of wire byte q: R.src + (q - R.data_w), as pointer
+        // arithmetic on the payload argument (global_* loads; a uintptr_t
+        // round trip made them flat loads, whose lgkmcnt share turned every
+        // scalar-load wait of the descriptor pipeline into a data-load wait)
+        s = (WSG_DIAG_ENC & 2) ? 0u
+                                : uint32_t((reinterpret_cast<uintptr_t>(R.src) + (lo - R.data_w)) & 15u);
         kw = key_rot(R.key, uint32_t(lo - R.pw));
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
             const uint64_t p = lo + (uint64_t(u) * 64 + lane) * CHUNK;
             const bool d = live && p < hi && p >= R.data_w && p + CHUNK <= R.end;
             dmask |= uint32_t(d) << u;
-            const uint8_t* a0 = reinterpret_cast<const uint8_t*>(sbase + p - s);
+            const uint8_t* a0 = R.src + (int64_t(p - R.data_w) - int64_t(s));
             a[u] = d ? (NT ? ld16nt(a0) : ld16(a0)) : v4u{0, 0, 0, 0};
         }
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
             const uint64_t p = lo + (uint64_t(u) * 64 + lane) * CHUNK;
-            const uint8_t* a0 = reinterpret_cast<const uint8_t*>(sbase + p - s);
+            const uint8_t* a0 = R.src + (int64_t(p - R.data_w) - int64_t(s));
             b[u] = ((dmask >> u) & 1u) && s ? ((NT && WSG_ENC_NT_HI) ? ld16nt(a0 + CHUNK) : ld16(a0 + CHUNK))
                                           : v4u{0, 0, 0, 0};
         }
@@ -1149,16 +1153,16 @@ __device__ __forceinline__ uint32_t fan_byte(const uint8_t* __restrict__ payload
 // hold a wanted byte, at most two.
 __device__ __forceinline__ v4u fan_window(const uint8_t* __restrict__ payload, uint64_t len, int64_t c)
 {
-    const intptr_t base = reinterpret_cast<intptr_t>(payload);
-    const intptr_t b = base + intptr_t(c);
-    const uint32_t s = uint32_t(b & 15);
-    const intptr_t a0 = b - intptr_t(s);
-    const intptr_t lo_valid = base, hi_valid = base + intptr_t(len);
+    // offsets relative to `payload`, loads through pointer arithmetic on it
+    // (global_* loads; a pointer rebuilt from an integer loads flat_*)
+    const uint32_t s = uint32_t((reinterpret_cast<uintptr_t>(payload) + uint64_t(c)) & 15u);
+    const int64_t r0 = c - int64_t(s);   // aligned block holding byte c, relative to payload
+    const int64_t n = int64_t(len);
     v4u lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
-    if (a0 < hi_valid && a0 + 16 > lo_valid)
-        lo = ld16(reinterpret_cast<const uint8_t*>(a0));
-    if (s != 0 && a0 + 16 < hi_valid && a0 + 32 > lo_valid)
-        hi = ld16(reinterpret_cast<const uint8_t*>(a0 + 16));
+    if (r0 < n && r0 + 16 > 0)
+        lo = ld16(payload + r0);
+    if (s != 0 && r0 + 16 < n && r0 + 32 > 0)
+        hi = ld16(payload + r0 + 16);
     return s ? funnel(lo, hi, s) : lo;
 }
 
@@ -1237,20 +1241,23 @@ __device__ __forceinline__ v4u fan_frame_bytes(const uint8_t* __restrict__ paylo
 static_assert(SMALL_F <= BLOCK && SCAN_ITEMS % SMALL_F == 0, "k_encode_small: one frame per lane, one scan block");
 
 struct SmallFrame {
-    uint64_t src;   // address of the first data byte
+    uint64_t src;   // offset of the first data byte in the payload arena (an
+                    // offset, not an address: loads through a pointer rebuilt
+                    // from an integer are flat loads)
     uint32_t key;
     uint32_t geo;   // head bytes (header + status) | header bytes << 8
 };
 
 // Bytes [o, o + 16) of a frame of fsize bytes (o < fsize), 0 past its end.
-__device__ __forceinline__ v4u small_bytes(v4u head, const SmallFrame& f, uint64_t fsize, uint64_t o)
+__device__ __forceinline__ v4u small_bytes(const uint8_t* __restrict__ payload, v4u head, const SmallFrame& f,
+                                          uint64_t fsize, uint64_t o)
 {
     const uint32_t data0 = f.geo & 0xFFu, hdr = f.geo >> 8;
     v4u out = shr_bytes(head, o);
     const uint64_t lo = o < data0 ? data0 - o : 0;   // chunk bytes [lo, hi) are payload
     const uint64_t hi = fsize - o < CHUNK ? fsize - o : CHUNK;
     if (lo < hi) {
-        const v4u w = fan_window(reinterpret_cast<const uint8_t*>(f.src), fsize - data0, int64_t(o) - int64_t(data0));
+        const v4u w = fan_window(payload + f.src, fsize - data0, int64_t(o) - int64_t(data0));
         out |= (w ^ key_rot(f.key, uint32_t(o - hdr))) & (low_bytes(hi) & ~low_bytes(lo));
     }
     return out;
@@ -1305,7 +1312,7 @@ __global__ __launch_bounds__(BLOCK) void k_encode_small(const uint8_t* __restric
             put_byte(h, g.hdr + 1, uint32_t(d.status & 0xFF) ^ key_byte(d.key, 1));
         }
         s_head[t] = h;
-        s_fr[t] = SmallFrame{reinterpret_cast<uintptr_t>(payload + d.src_off), d.key,
+        s_fr[t] = SmallFrame{d.src_off, d.key,
                              (g.hdr + g.prefix) | (g.hdr << 8)};
     }
     uint64_t before = 0, all = 0;
@@ -1358,9 +1365,9 @@ __global__ __launch_bounds__(BLOCK) void k_encode_small(const uint8_t* __restric
                 break;
             const uint64_t fsize = s_off[j + 1] - off;
             if (p >= off)
-                w |= small_bytes(s_head[j], s_fr[j], fsize, p - off);
+                w |= small_bytes(payload, s_head[j], s_fr[j], fsize, p - off);
             else
-                w |= shl_bytes(small_bytes(s_head[j], s_fr[j], fsize, 0), off - p);
+                w |= shl_bytes(small_bytes(payload, s_head[j], s_fr[j], fsize, 0), off - p);
         }
         if (p >= r_lo && p + CHUNK <= r_hi) {
             st16nt(wire + p, w);
