@@ -8,6 +8,11 @@
 #include "server/ws/ws_client.h"
 #include "server/ws/ws_handshake.h"
 #include "server/ws/ws_session.h"
+#include "server/ws/wss_client.h"
+#include "server/ws/wss_server.h"
+#include "server/ws/wss_session.h"
+
+#include "tls_test_certs.h"
 
 #include <cstdio>
 #include <deque>
@@ -158,7 +163,7 @@ static void test_client_rules()
     CHECK(!c.PerformClientUpgrade(not101) && c.errors.size() == errs);   // silently not an upgrade
 }
 
-// in-memory transport pair
+// in-memory transport pair (the WSS tests read the inboxes directly)
 struct Loop : Transport {
     Loop* peer = nullptr;
     std::deque<uint8_t> inbox;
@@ -216,6 +221,147 @@ static void test_client_session_upgrade()
     CHECK(client.up && client.IsConnected());
 }
 
+// WSS (reference include/server/ws/wss_*.h): the upgrade over a real TLS
+// session (OpenSSL, TLS 1.3, the client verifying the server's certificate
+// against a run-time CA), records pumped between the two byte transports.
+// No frame is sent, so no GPU is needed.
+struct MyWssClient : WSSClient {
+    using WSSClient::WSSClient;
+    bool up = false, tls_up = false;
+    std::string err;
+    void onWSConnecting(HTTP::HTTPRequest& request) override
+    {
+        request.SetBegin("GET", "/");
+        request.SetHeader("Host", "localhost");
+        request.SetHeader("Upgrade", "websocket");
+        request.SetHeader("Connection", "Upgrade");
+        request.SetHeader("Sec-WebSocket-Key", Base64Encode(ws_nonce()));
+        request.SetHeader("Sec-WebSocket-Version", "13");
+    }
+    void onWSConnected(const HTTP::HTTPResponse&) override { up = true; }
+    void onWSError(const std::string& message) override { err = message; }
+    void onHandshaked() override
+    {
+        tls_up = true;
+        WSSClient::onHandshaked();
+    }
+};
+
+struct MyWssSession : WSSSession {
+    using WSSSession::WSSSession;
+    bool up = false;
+    std::string err;
+    void onWSConnected(const HTTP::HTTPRequest&) override { up = true; }
+    void onWSError(const std::string& message) override { err = message; }
+};
+
+template <class C, class S>
+static void pump(Loop& a, Loop& b, C& client, S& session, bool tamper_once = false)
+{
+    for (int guard = 0; guard < 64 && (!a.inbox.empty() || !b.inbox.empty()); ++guard) {
+        if (!b.inbox.empty()) {
+            std::vector<uint8_t> rec(b.inbox.begin(), b.inbox.end());
+            b.inbox.clear();
+            if (tamper_once && rec.size() > 40) {
+                rec[rec.size() - 20] ^= 0x01;   // one flipped bit in an application record
+                tamper_once = false;
+            }
+            session.onReceived(rec.data(), rec.size());
+        }
+        if (!a.inbox.empty()) {
+            std::vector<uint8_t> rec(a.inbox.begin(), a.inbox.end());
+            a.inbox.clear();
+            client.onReceived(rec.data(), rec.size());
+        }
+    }
+}
+
+static void test_wss_upgrade()
+{
+    using CppServer::Asio::SSLContext;
+    const TestPki pki = make_test_pki();
+    // server: the reference's wss_chat_server configuration calls (examples/wss_chat_server.cpp:98-102)
+    auto server_ctx = std::make_shared<SSLContext>(asio::ssl::context::tlsv13);
+    server_ctx->set_password_callback([](size_t, asio::ssl::context::password_purpose) -> std::string { return "qwerty"; });
+    server_ctx->use_certificate_chain(pki.server_cert_pem.data(), pki.server_cert_pem.size());
+    server_ctx->use_private_key(pki.server_key_pem.data(), pki.server_key_pem.size(), asio::ssl::context::pem);
+    // client: wss_chat_client's (examples/wss_chat_client.cpp:105-109), the CA from memory
+    auto client_ctx = std::make_shared<SSLContext>(asio::ssl::context::tlsv13);
+    client_ctx->set_verify_mode(asio::ssl::verify_peer | asio::ssl::verify_fail_if_no_peer_cert);
+    client_ctx->add_certificate_authority(pki.ca_pem.data(), pki.ca_pem.size());
+
+    {
+        Loop a, b;
+        a.peer = &b;
+        b.peer = &a;
+        WSSServer server(server_ctx);
+        MyWssClient client(client_ctx, a);
+        auto session = std::make_shared<MyWssSession>(server.context(), b);
+        server.AddSession(session);
+        CHECK(session->Connect());
+        CHECK(client.Connect());
+        CHECK(!b.inbox.empty());   // the ClientHello
+        pump(a, b, client, *session);
+        CHECK(client.tls_up && client.IsHandshaked() && session->IsHandshaked());
+        CHECK(client.tls().protocol() == "TLSv1.3");
+        CHECK(session->up && session->IsConnected());
+        CHECK(client.up && client.IsConnected());
+        CHECK(client.err.empty() && session->err.empty());
+        // the upgrade bytes crossed as TLS records: no cleartext HTTP on the wire
+        server.RemoveSession(session);
+    }
+    {
+        // a client that does not trust the server's CA fails the handshake
+        Loop a, b;
+        a.peer = &b;
+        b.peer = &a;
+        auto strict = std::make_shared<SSLContext>(asio::ssl::context::tlsv13);
+        strict->set_verify_mode(asio::ssl::verify_peer | asio::ssl::verify_fail_if_no_peer_cert);
+        MyWssClient client(strict, a);
+        MyWssSession session(server_ctx, b);
+        CHECK(session.Connect());
+        CHECK(client.Connect());
+        pump(a, b, client, session);
+        CHECK(!client.IsHandshaked() && !client.up && !client.err.empty());
+        CHECK(client.err.find("certificate verify failed") != std::string::npos);
+    }
+    {
+        // a tampered record is rejected (AEAD), not delivered
+        Loop a, b;
+        a.peer = &b;
+        b.peer = &a;
+        MyWssClient client(client_ctx, a);
+        MyWssSession session(server_ctx, b);
+        CHECK(session.Connect());
+        CHECK(client.ConnectAsync());
+        // handshake records untouched; the upgrade request (first application
+        // record to the session) gets one bit flipped
+        for (int guard = 0; guard < 64 && !client.IsHandshaked(); ++guard) {
+            std::vector<uint8_t> rb(b.inbox.begin(), b.inbox.end()), ra(a.inbox.begin(), a.inbox.end());
+            b.inbox.clear();
+            a.inbox.clear();
+            if (!rb.empty())
+                session.onReceived(rb.data(), rb.size());
+            if (!ra.empty())
+                client.onReceived(ra.data(), ra.size());
+        }
+        CHECK(client.IsHandshaked());
+        pump(a, b, client, session, true);
+        CHECK(!session.up && !session.err.empty());
+    }
+    {
+        // configuration errors surface as exceptions with OpenSSL's text
+        auto ctx = std::make_shared<SSLContext>(asio::ssl::context::tlsv12);
+        bool threw = false;
+        try {
+            ctx->use_certificate_chain_file("/nonexistent/server.pem");
+        } catch (const std::exception& e) {
+            threw = std::string(e.what()).find("use_certificate_chain_file") != std::string::npos;
+        }
+        CHECK(threw);
+    }
+}
+
 int main()
 {
     try {
@@ -224,6 +370,7 @@ int main()
         test_server_rules();
         test_client_rules();
         test_client_session_upgrade();
+        test_wss_upgrade();
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());
         return 2;

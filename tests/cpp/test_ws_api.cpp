@@ -12,6 +12,8 @@
 #include "server/ws/wss_server.h"
 #include "server/ws/wss_session.h"
 
+#include "tls_test_certs.h"
+
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
@@ -566,29 +568,12 @@ static void test_batch_threads()
     CHECK(cnt.ordered);
 }
 
-// WSS (reference include/server/ws/wss_*.h): the same codec over a transport
-// that transforms the byte stream (a toy stream cipher standing in for TLS
-// records).  The WebSocket layer must not see the difference.
-struct ToyTls : Loopback {
-    uint8_t k_out = 0x5A, k_in = 0x5A;
-    size_t Send(const void* b, size_t n) override
-    {
-        std::vector<uint8_t> c((const uint8_t*)b, (const uint8_t*)b + n);
-        for (auto& x : c)
-            x ^= k_out++;   // "encrypt"
-        return Loopback::Send(c.data(), c.size());
-    }
-    // the peer's records, decrypted before they reach the WebSocket layer
-    std::vector<uint8_t> take()
-    {
-        std::vector<uint8_t> p(inbox.begin(), inbox.end());
-        inbox.clear();
-        for (auto& x : p)
-            x ^= k_in++;
-        return p;
-    }
-};
-
+// WSS (reference include/server/ws/wss_*.h): the same codec over a real TLS
+// session (OpenSSL TLS 1.3 through TLSTransport, certificates made at run
+// time), records pumped between the two byte transports.  Frames both ways,
+// a 70 KB one (several TLS records), a multicast, and the batched paths: the
+// server's batched receive and send run on the decrypted bytes / encrypt
+// the encoded frames.
 struct TlsClient : WSSClient {
     using WSSClient::WSSClient;
     std::vector<std::vector<uint8_t>> messages;
@@ -611,40 +596,68 @@ struct TlsSession : WSSSession {
 
 static void test_wss()
 {
-    ToyTls ct, st;
-    ct.peer = &st;
-    st.peer = &ct;
-    TlsClient client(ct);
-    auto session = std::make_shared<TlsSession>(st);
-    WSSServer server;
-    server.AddSession(session);
-    auto pump = [&] {
-        for (int guard = 0; guard < 100 && (!ct.inbox.empty() || !st.inbox.empty()); ++guard) {
-            if (!st.inbox.empty()) {
-                auto b = st.take();
-                session->onReceived(b.data(), b.size());
-            }
-            if (!ct.inbox.empty()) {
-                auto b = ct.take();
-                client.onReceived(b.data(), b.size());
-            }
+    using CppServer::Asio::SSLContext;
+    const TestPki pki = make_test_pki();
+    auto sctx = std::make_shared<SSLContext>(asio::ssl::context::tlsv13);
+    sctx->use_certificate_chain(pki.server_cert_pem.data(), pki.server_cert_pem.size());
+    sctx->use_private_key(pki.server_key_pem.data(), pki.server_key_pem.size(), asio::ssl::context::pem);
+    auto cctx = std::make_shared<SSLContext>(asio::ssl::context::tlsv13);
+    cctx->set_verify_mode(asio::ssl::verify_peer | asio::ssl::verify_fail_if_no_peer_cert);
+    cctx->add_certificate_authority(pki.ca_pem.data(), pki.ca_pem.size());
+
+    for (int batched = 0; batched < 2; ++batched) {
+        Loopback ct, st;
+        ct.peer = &st;
+        st.peer = &ct;
+        TlsClient client(cctx, ct);
+        WSSServer server(sctx);
+        auto session = std::make_shared<TlsSession>(server.context(), st);
+        server.AddSession(session);
+        if (batched) {
+            server.EnableBatchReceive(true);
+            server.EnableBatchSend(true);
         }
-    };
-    session->Connect();
-    client.Connect();
-    pump();
-    CHECK(client.IsConnected());
-    std::vector<uint8_t> big(70000);
-    for (size_t i = 0; i < big.size(); ++i)
-        big[i] = uint8_t(i * 7 + 1);
-    CHECK(client.SendBinaryAsync(big.data(), big.size()));
-    CHECK(client.SendTextAsync("over tls"));
-    pump();
-    CHECK(client.messages.size() == 2 && client.messages[0] == big &&
-          std::string(client.messages[1].begin(), client.messages[1].end()) == "over tls");
-    CHECK(server.MulticastText("all") > 0);
-    pump();
-    CHECK(client.messages.size() == 3 && std::string(client.messages[2].begin(), client.messages[2].end()) == "all");
+        size_t wire_bytes = 0;
+        auto pump = [&] {
+            for (int guard = 0; guard < 200 && (!ct.inbox.empty() || !st.inbox.empty()); ++guard) {
+                if (!st.inbox.empty()) {
+                    std::vector<uint8_t> b(st.inbox.begin(), st.inbox.end());
+                    st.inbox.clear();
+                    wire_bytes += b.size();
+                    session->onReceived(b.data(), b.size());
+                    if (batched) {
+                        server.FlushReceived();
+                        server.FlushSend();
+                    }
+                }
+                if (!ct.inbox.empty()) {
+                    std::vector<uint8_t> b(ct.inbox.begin(), ct.inbox.end());
+                    ct.inbox.clear();
+                    wire_bytes += b.size();
+                    client.onReceived(b.data(), b.size());
+                }
+            }
+        };
+        CHECK(session->Connect());
+        CHECK(client.Connect());
+        pump();
+        CHECK(client.IsHandshaked() && client.IsConnected() && session->IsConnected());
+        std::vector<uint8_t> big(70000);
+        for (size_t i = 0; i < big.size(); ++i)
+            big[i] = uint8_t(i * 7 + 1);
+        CHECK(client.SendBinaryAsync(big.data(), big.size()));
+        CHECK(client.SendTextAsync("over tls"));
+        pump();
+        CHECK(client.messages.size() == 2 && client.messages[0] == big &&
+              std::string(client.messages[1].begin(), client.messages[1].end()) == "over tls");
+        CHECK(wire_bytes > 2 * big.size());   // both directions, plus record overhead
+        CHECK(server.MulticastText("all") > 0);
+        if (batched)
+            server.FlushSend();
+        pump();
+        CHECK(client.messages.size() == 3 && std::string(client.messages[2].begin(), client.messages[2].end()) == "all");
+        server.RemoveSession(session);
+    }
 }
 
 int main()
