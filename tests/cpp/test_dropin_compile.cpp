@@ -103,4 +103,26 @@ public:
 
 [[maybe_unused]] void use_wss(WSSClient& c, WSSServer& s) { (void)c.SendTextAsync("tls"); (void)s.MulticastText("tls"); }
 
+// the reference's SSL context set-up, verbatim in form
+// (examples/wss_chat_server.cpp:98-102, examples/wss_chat_client.cpp:105-109)
+[[maybe_unused]] std::shared_ptr<CppServer::Asio::SSLContext> server_context()
+{
+    auto context = std::make_shared<CppServer::Asio::SSLContext>(asio::ssl::context::tlsv13);
+    context->set_password_callback([](size_t max_length, asio::ssl::context::password_purpose purpose) -> std::string { return "qwerty"; });
+    context->use_certificate_chain_file("../tools/certificates/server.pem");
+    context->use_private_key_file("../tools/certificates/server.pem", asio::ssl::context::pem);
+    context->use_tmp_dh_file("../tools/certificates/dh4096.pem");
+    return context;
+}
+
+[[maybe_unused]] std::shared_ptr<CppServer::Asio::SSLContext> client_context()
+{
+    auto context = std::make_shared<CppServer::Asio::SSLContext>(asio::ssl::context::tlsv13);
+    context->set_default_verify_paths();
+    context->set_root_certs();
+    context->set_verify_mode(asio::ssl::verify_peer | asio::ssl::verify_fail_if_no_peer_cert);
+    context->load_verify_file("../tools/certificates/ca.pem");
+    return context;
+}
+
 } // namespace
