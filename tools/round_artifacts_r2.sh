@@ -24,7 +24,7 @@ declare -A ARGS=(
     [c5]="--config c5"
 )
 declare -A STEPS=([c2]=200 [c3]=10 [c4]=50 [c4x16]=20 [c5]=10)
-for c in c2 c3 c4 c4x16 c5; do
+for c in ${CFGS:-c2 c3 c4 c4x16 c5}; do
     run "bench_$c" 600 python bench.py ${ARGS[$c]} --steps ${STEPS[$c]} --warmup 3
     run "trace_$c" 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$c" -o run --output-format csv -- \
         python bench.py ${ARGS[$c]} --steps ${STEPS[$c]} --warmup 3 --no-cpu --no-extras
@@ -33,7 +33,7 @@ for c in c2 c3 c4 c4x16 c5; do
             python bench.py ${ARGS[$c]} --steps 5 --warmup 1 --no-cpu --no-extras
     done
 done
-for k in FETCH_SIZE WRITE_SIZE; do
+[ "${CALIB:-1}" = 1 ] && for k in FETCH_SIZE WRITE_SIZE; do
     run "pmc_calib_$k" 300 rocprofv3 --pmc $k -d "$OUT/pmc_calib_$k" -o run --output-format csv -- \
         tools/_build/membench 1024 calib
 done
