@@ -495,7 +495,8 @@ def echo_c1_leg(seconds=3.0, timeout=120):
     over in-memory transports (tools/_build/bench_echo, product library only;
     no sockets: the transport is out of scope).  per_read = the API's default
     (each read one batch scope), tick = one scope per event-loop pass,
-    per_call = automatic batching off (one GPU round trip per masked frame).
+    per_call = automatic batching off (one GPU round trip per masked frame);
+    wss_* = the same through WSSClient / WSSSession over TLS 1.3 (wss_echo).
     Metric as ws_echo_client.cpp:191-201 (messages = echoed bytes / size)."""
     import subprocess
 
@@ -506,16 +507,22 @@ def echo_c1_leg(seconds=3.0, timeout=120):
     legs = (("per_read_1c", ["per_read", "1", "1", "1000", "32"]),
             ("per_read_100c_4t", ["per_read", "100", "4", "1000", "32"]),
             ("tick_100c_1t", ["tick", "100", "1", "1000", "32"]),
-            ("per_call_1c", ["per_call", "1", "1", "1000", "32"]))
+            ("per_call_1c", ["per_call", "1", "1", "1000", "32"]),
+            # wss_echo (performance/wss_echo_client.cpp): the same loop through
+            # WSSClient / WSSSession over TLS 1.3 (OpenSSL record encryption)
+            ("wss_per_read_1c", ["per_read", "1", "1", "1000", "32"]),
+            ("wss_per_read_100c_4t", ["per_read", "100", "4", "1000", "32"]))
     for leg, args in legs:
-        r = subprocess.run([exe] + args + [str(seconds)], capture_output=True, text=True, timeout=timeout)
+        extra = ["tls"] if leg.startswith("wss_") else []
+        r = subprocess.run([exe] + args + [str(seconds)] + extra, capture_output=True, text=True, timeout=timeout)
         if r.returncode != 0:
             out[leg] = {"error": (r.stderr or r.stdout).strip()[-300:]}
             continue
         d = json.loads(r.stdout.strip().splitlines()[-1])
         out[leg] = {k: d[k] for k in ("msg_per_s", "MiB_per_s", "latency_ns", "total_messages", "payload_ok")}
     out["reference_published"] = {"msg_per_s_1c_1t": 160448, "msg_per_s_100c_4t": 594328,
-                                  "hardware": "i7-4790K, loopback sockets (README.md:3312-3352)"}
+                                  "wss_msg_per_s_1c_1t": 203343, "wss_msg_per_s_100c_4t": 818230,
+                                  "hardware": "i7-4790K, loopback sockets (README.md:3312-3352, 3356-3396)"}
     return out
 
 

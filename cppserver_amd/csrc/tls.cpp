@@ -329,13 +329,17 @@ bool TLSTransport::Feed(const void* buffer, size_t size, const Plain& plain, con
     bool just_handshaked = false;
     {
         std::lock_guard<std::recursive_mutex> g(_lock);
+        ++_feeding;
         if (_failed)
             return false;
-        if (size && BIO_write(_rbio, buffer, int(size)) != int(size))
+        if (size && BIO_write(_rbio, buffer, int(size)) != int(size)) {
+            --_feeding;
             return fail("BIO_write");
+        }
         if (!_handshaked) {
             just_handshaked = step_handshake();
             if (_failed) {
+                --_feeding;
                 out = drain_records();   // the alert, if any
                 if (!out.empty())
                     _lower.SendAsync(out.data(), out.size());
@@ -361,10 +365,24 @@ bool TLSTransport::Feed(const void* buffer, size_t size, const Plain& plain, con
     }
     if (!out.empty())
         _lower.SendAsync(out.data(), out.size());
+    // what the callbacks send (an echo, the upgrade after the handshake)
+    // is held back and encrypted once they return: one SSL_write, full
+    // records, instead of one record per frame
     if (just_handshaked && handshaked)
         handshaked();
     if (!text.empty() && plain)
         plain(text.data(), text.size());
+    std::vector<uint8_t> rec;
+    {
+        std::lock_guard<std::recursive_mutex> g(_lock);
+        if (--_feeding == 0 && !_out_plain.empty()) {
+            std::vector<uint8_t> p;
+            p.swap(_out_plain);
+            encrypt(p.data(), p.size(), rec);
+        }
+    }
+    if (!rec.empty())
+        _lower.SendAsync(rec.data(), rec.size());
     return !_failed;
 }
 
@@ -388,11 +406,25 @@ size_t TLSTransport::encrypt(const void* buffer, size_t size, std::vector<uint8_
     return done;
 }
 
+size_t TLSTransport::encrypt_after_pending(const void* buffer, size_t size, std::vector<uint8_t>& records)
+{
+    std::lock_guard<std::recursive_mutex> g(_lock);
+    if (!_out_plain.empty()) {   // bytes held back by a feed in progress go first
+        std::vector<uint8_t> p;
+        p.swap(_out_plain);
+        if (encrypt(p.data(), p.size(), records) != p.size())
+            return 0;
+    }
+    std::vector<uint8_t> more;
+    const size_t n = encrypt(buffer, size, more);
+    records.insert(records.end(), more.begin(), more.end());
+    return n;
+}
+
 size_t TLSTransport::Send(const void* buffer, size_t size)
 {
     std::vector<uint8_t> rec;
-    const size_t n = encrypt(buffer, size, rec);
-    if (n != size)
+    if (encrypt_after_pending(buffer, size, rec) != size)
         return 0;
     return rec.empty() || _lower.Send(rec.data(), rec.size()) == rec.size() ? size : 0;
 }
@@ -400,16 +432,25 @@ size_t TLSTransport::Send(const void* buffer, size_t size)
 size_t TLSTransport::Send(const void* buffer, size_t size, const CppCommon::Timespan& timeout)
 {
     std::vector<uint8_t> rec;
-    const size_t n = encrypt(buffer, size, rec);
-    if (n != size)
+    if (encrypt_after_pending(buffer, size, rec) != size)
         return 0;
     return rec.empty() || _lower.Send(rec.data(), rec.size(), timeout) == rec.size() ? size : 0;
 }
 
 bool TLSTransport::SendAsync(const void* buffer, size_t size)
 {
+    {
+        std::lock_guard<std::recursive_mutex> g(_lock);
+        if (_failed || !_handshaked)
+            return false;
+        if (_feeding) {   // inside a feed's callbacks: encrypted when they return
+            const uint8_t* p = static_cast<const uint8_t*>(buffer);
+            _out_plain.insert(_out_plain.end(), p, p + size);
+            return true;
+        }
+    }
     std::vector<uint8_t> rec;
-    if (encrypt(buffer, size, rec) != size)
+    if (encrypt_after_pending(buffer, size, rec) != size)
         return false;
     return rec.empty() || _lower.SendAsync(rec.data(), rec.size());
 }

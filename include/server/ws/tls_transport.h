@@ -12,7 +12,10 @@
  * flush hands each encoded frame to SendAsync, which encrypts it.
  *
  *  - Send / SendAsync: plaintext in, records out through lower.Send /
- *    lower.SendAsync (one call per Send, after SSL_write).
+ *    lower.SendAsync (one call per Send, after SSL_write).  SendAsync calls
+ *    made from inside Feed's callbacks (an echo, a batch flush at the end
+ *    of a read) are held back and encrypted together when the callbacks
+ *    return: full 16 KiB records instead of one record per frame.
  *  - Feed: records read from `lower` (what its owner's onReceived gets);
  *    advances the handshake, hands decrypted bytes to `plain` and calls
  *    `handshaked` once when the handshake completes.
@@ -92,6 +95,8 @@ private:
     std::string _error;
     std::vector<uint8_t> _pending;   // plaintext decrypted by Receive beyond what was asked
     size_t _pending_at{0};
+    std::vector<uint8_t> _out_plain;   // SendAsync bytes held back while a Feed runs its callbacks
+    int _feeding{0};
     mutable std::recursive_mutex _lock;
 
     // encrypted bytes waiting in _wbio (handshake records, application records)
@@ -100,6 +105,7 @@ private:
     bool step_handshake();
     bool fail(const char* what);
     size_t encrypt(const void* buffer, size_t size, std::vector<uint8_t>& records);
+    size_t encrypt_after_pending(const void* buffer, size_t size, std::vector<uint8_t>& records);
 };
 
 } // namespace WS

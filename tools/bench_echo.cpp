@@ -24,12 +24,21 @@
 //   per_call  automatic batching off ($WSG_AUTO_BATCH=0 semantics): one GPU
 //             round trip per masked frame, the round-1 path.
 //
-//   bench_echo MODE CLIENTS THREADS MESSAGES SIZE SECONDS
+//   bench_echo MODE CLIENTS THREADS MESSAGES SIZE SECONDS [tls]
+// `tls`: the reference's wss_echo (performance/wss_echo_client.cpp /
+// wss_echo_server.cpp): WSSClient / WSSSession over TLS 1.3 (OpenSSL,
+// certificates made at start-up), the same echo loop.
 // Prints one JSON object.  Links the product library only.
 #include "server/ws/ws_batch.h"
 #include "server/ws/ws_client.h"
 #include "server/ws/ws_handshake.h"
 #include "server/ws/ws_session.h"
+#include "server/ws/wss_client.h"
+#include "server/ws/wss_session.h"
+
+#include "../tests/cpp/tls_test_certs.h"
+
+#include <functional>
 
 #include <atomic>
 #include <chrono>
@@ -71,16 +80,21 @@ struct Pipe : Transport {
 std::vector<uint8_t> g_message;
 std::atomic<bool> g_stop{false};
 
-struct EchoSession : WSSession {
-    using WSSession::WSSession;
-    void onWSReceived(const void* buffer, size_t size) override { SendBinaryAsync(buffer, size); }
+template <class Base>
+struct EchoSession : Base {
+    using Base::Base;
+    void onWSReceived(const void* buffer, size_t size) override { this->SendBinaryAsync(buffer, size); }
 };
 
-struct EchoClient : WSClient {
-    EchoClient(Transport& t, size_t messages) : WSClient(t), _messages(messages) {}
+template <class Base>
+struct EchoClient : Base {
+    template <class... A>
+    explicit EchoClient(size_t messages, A&&... a) : Base(std::forward<A>(a)...), _messages(messages)
+    {
+    }
     uint64_t total_bytes = 0;
     uint64_t bad = 0;
-    void SendMessage() { SendBinaryAsync(g_message.data(), g_message.size()); }
+    void SendMessage() { this->SendBinaryAsync(g_message.data(), g_message.size()); }
     void onWSConnecting(CppServer::HTTP::HTTPRequest& request) override
     {
         request.SetBegin("GET", "/");
@@ -88,7 +102,7 @@ struct EchoClient : WSClient {
         request.SetHeader("Origin", "http://localhost");
         request.SetHeader("Upgrade", "websocket");
         request.SetHeader("Connection", "Upgrade");
-        request.SetHeader("Sec-WebSocket-Key", Base64Encode(ws_nonce()));
+        request.SetHeader("Sec-WebSocket-Key", Base64Encode(this->ws_nonce()));
         request.SetHeader("Sec-WebSocket-Protocol", "chat, superchat");
         request.SetHeader("Sec-WebSocket-Version", "13");
     }
@@ -118,11 +132,28 @@ private:
     size_t _messages;
 };
 
+// one connection: WS or WSS endpoints behind the same calls (onReceived is
+// the TLS record path on the WSS classes, so it is bound to the concrete type)
 struct Conn {
     Pipe ct, st;
-    std::unique_ptr<EchoClient> client;
-    std::unique_ptr<EchoSession> session;
+    std::shared_ptr<void> client, session;
+    std::function<void(const void*, size_t)> client_rx, session_rx;
+    std::function<void()> connect;
+    std::function<uint64_t()> total_bytes, bad;
 };
+
+template <class C, class S>
+void bind(Conn& cn, std::shared_ptr<C> c, std::shared_ptr<S> s)
+{
+    cn.client_rx = [c](const void* b, size_t n) { c->onReceived(b, n); };
+    cn.session_rx = [s](const void* b, size_t n) { s->onReceived(b, n); };
+    cn.connect = [c] { c->Connect(); };
+    cn.total_bytes = [c] { return c->total_bytes; };
+    cn.bad = [c] { return c->bad; };
+    s->Connect();
+    cn.client = c;
+    cn.session = s;
+}
 
 double seconds(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 
@@ -144,10 +175,22 @@ bool read_all(Pipe& p, std::vector<uint8_t>& buf, F fn)
 int main(int argc, char** argv)
 {
     if (argc < 7) {
-        std::fprintf(stderr, "usage: %s per_read|tick|per_call CLIENTS THREADS MESSAGES SIZE SECONDS\n", argv[0]);
+        std::fprintf(stderr, "usage: %s per_read|tick|per_call CLIENTS THREADS MESSAGES SIZE SECONDS [tls]\n", argv[0]);
         return 2;
     }
     const std::string mode = argv[1];
+    const bool tls = argc > 7 && std::string(argv[7]) == "tls";
+    std::shared_ptr<CppServer::Asio::SSLContext> cctx, sctx;
+    if (tls) {
+        using CppServer::Asio::SSLContext;
+        const TestPki pki = make_test_pki();
+        sctx = std::make_shared<SSLContext>(SSLContext::tlsv13);
+        sctx->use_certificate_chain(pki.server_cert_pem.data(), pki.server_cert_pem.size());
+        sctx->use_private_key(pki.server_key_pem.data(), pki.server_key_pem.size(), SSLContext::pem);
+        cctx = std::make_shared<SSLContext>(SSLContext::tlsv13);
+        cctx->set_verify_mode(CppServer::Asio::verify_peer | CppServer::Asio::verify_fail_if_no_peer_cert);
+        cctx->add_certificate_authority(pki.ca_pem.data(), pki.ca_pem.size());
+    }
     const int clients = std::atoi(argv[2]), threads = std::max(1, std::atoi(argv[3]));
     const size_t messages = std::strtoull(argv[4], nullptr, 10), size = std::strtoull(argv[5], nullptr, 10);
     const double secs = std::atof(argv[6]);
@@ -170,9 +213,12 @@ int main(int argc, char** argv)
                 auto cn = std::make_unique<Conn>();
                 cn->ct.peer = &cn->st;
                 cn->st.peer = &cn->ct;
-                cn->client = std::make_unique<EchoClient>(cn->ct, messages);
-                cn->session = std::make_unique<EchoSession>(cn->st);
-                cn->session->Connect();
+                if (tls)
+                    bind(*cn, std::make_shared<EchoClient<WSSClient>>(messages, cctx, cn->ct),
+                         std::make_shared<EchoSession<WSSSession>>(sctx, cn->st));
+                else
+                    bind(*cn, std::make_shared<EchoClient<WSClient>>(messages, cn->ct),
+                         std::make_shared<EchoSession<WSSession>>(cn->st));
                 mine.push_back(cn.get());
                 conns[size_t(c)] = std::move(cn);
             }
@@ -181,7 +227,7 @@ int main(int argc, char** argv)
                 std::this_thread::yield();
             const auto t0 = Clock::now();
             for (Conn* c : mine)
-                c->client->Connect();
+                c->connect();
             std::vector<uint8_t> buf;
             uint64_t polls = 0;
             for (;;) {
@@ -193,8 +239,8 @@ int main(int argc, char** argv)
                     if (mode == "tick")
                         tick = std::make_unique<BatchScope>();
                     for (Conn* c : mine) {
-                        any |= read_all(c->st, buf, [&](const void* b, size_t n) { c->session->onReceived(b, n); });
-                        any |= read_all(c->ct, buf, [&](const void* b, size_t n) { c->client->onReceived(b, n); });
+                        any |= read_all(c->st, buf, c->session_rx);
+                        any |= read_all(c->ct, buf, c->client_rx);
                     }
                 }
                 ++polls;
@@ -205,8 +251,8 @@ int main(int argc, char** argv)
             }
             elapsed[size_t(t)] = seconds(t0, Clock::now());
             for (Conn* c : mine) {
-                bytes[size_t(t)] += c->client->total_bytes;
-                bad[size_t(t)] += c->client->bad;
+                bytes[size_t(t)] += c->total_bytes();
+                bad[size_t(t)] += c->bad();
             }
         } catch (const std::exception& e) {
             errors[size_t(t)] = e.what();
@@ -231,10 +277,10 @@ int main(int argc, char** argv)
         el = std::max(el, elapsed[size_t(t)]);
     }
     const uint64_t msgs = size ? total / size : 0;
-    std::printf("{\"mode\": \"%s\", \"clients\": %d, \"threads\": %d, \"messages_in_flight\": %zu, \"size\": %zu, "
+    std::printf("{\"mode\": \"%s\", \"tls\": %s, \"clients\": %d, \"threads\": %d, \"messages_in_flight\": %zu, \"size\": %zu, "
                 "\"seconds\": %.3f, \"total_messages\": %llu, \"msg_per_s\": %.0f, \"MiB_per_s\": %.3f, "
                 "\"latency_ns\": %.1f, \"payload_ok\": %s}\n",
-                mode.c_str(), clients, threads, messages, size, el, (unsigned long long)msgs, msgs / el,
+                mode.c_str(), tls ? "true" : "false", clients, threads, messages, size, el, (unsigned long long)msgs, msgs / el,
                 total / el / (1 << 20), msgs ? el * 1e9 / double(msgs) : 0.0, total_bad == 0 ? "true" : "false");
     return 0;
 }
