@@ -14,6 +14,7 @@
 
 #include "tls_test_certs.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <deque>
 #include <string>
@@ -348,6 +349,39 @@ static void test_wss_upgrade()
         CHECK(client.IsHandshaked());
         pump(a, b, client, session, true);
         CHECK(!session.up && !session.err.empty());
+    }
+    {
+        // records cut at random points (partial records, several per read):
+        // the TLS handshake and the upgrade complete
+        Loop a, b;
+        a.peer = &b;
+        b.peer = &a;
+        MyWssClient client(client_ctx, a);
+        MyWssSession session(server_ctx, b);
+        CHECK(session.Connect());
+        CHECK(client.Connect());
+        uint64_t rng = 12345;
+        auto next = [&rng]() {
+            rng ^= rng << 13;
+            rng ^= rng >> 7;
+            rng ^= rng << 17;
+            return rng;
+        };
+        auto dribble = [&](Loop& from, auto& to) {
+            std::vector<uint8_t> rec(from.inbox.begin(), from.inbox.end());
+            from.inbox.clear();
+            for (size_t at = 0; at < rec.size();) {
+                const size_t n = std::min<size_t>(rec.size() - at, 1 + next() % 700);
+                to.onReceived(rec.data() + at, n);
+                at += n;
+            }
+        };
+        for (int guard = 0; guard < 64 && (!a.inbox.empty() || !b.inbox.empty()); ++guard) {
+            dribble(b, session);
+            dribble(a, client);
+        }
+        CHECK(client.up && session.up && client.err.empty() && session.err.empty());
+        // (frames through TLS under random splits: test_ws_api.cpp, GPU)
     }
     {
         // configuration errors surface as exceptions with OpenSSL's text

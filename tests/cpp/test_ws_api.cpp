@@ -14,6 +14,7 @@
 
 #include "tls_test_certs.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
@@ -657,6 +658,54 @@ static void test_wss()
         pump();
         CHECK(client.messages.size() == 3 && std::string(client.messages[2].begin(), client.messages[2].end()) == "all");
         server.RemoveSession(session);
+    }
+
+    // records cut at random points both ways (partial records, several per
+    // read), 60 messages of 0-5000 bytes echoed: same messages, same order
+    {
+        Loopback ct, st;
+        ct.peer = &st;
+        st.peer = &ct;
+        TlsClient client(cctx, ct);
+        auto session = std::make_shared<TlsSession>(sctx, st);
+        uint64_t rng = 777;
+        auto next = [&rng]() {
+            rng ^= rng << 13;
+            rng ^= rng >> 7;
+            rng ^= rng << 17;
+            return rng;
+        };
+        auto dribble = [&](Loopback& from, auto&& feed) {
+            std::vector<uint8_t> rec(from.inbox.begin(), from.inbox.end());
+            from.inbox.clear();
+            for (size_t at = 0; at < rec.size();) {
+                const size_t n = std::min<size_t>(rec.size() - at, 1 + next() % 900);
+                feed(rec.data() + at, n);
+                at += n;
+            }
+        };
+        auto pump = [&] {
+            for (int guard = 0; guard < 400 && (!ct.inbox.empty() || !st.inbox.empty()); ++guard) {
+                dribble(st, [&](const void* p, size_t n) { session->onReceived(p, n); });
+                dribble(ct, [&](const void* p, size_t n) { client.onReceived(p, n); });
+            }
+        };
+        CHECK(session->Connect());
+        CHECK(client.Connect());
+        pump();
+        CHECK(client.IsConnected() && session->IsConnected());
+        std::vector<std::vector<uint8_t>> sent;
+        for (int i = 0; i < 60; ++i) {
+            std::vector<uint8_t> m(size_t(next() % 5000));
+            for (auto& x : m)
+                x = uint8_t(next());
+            sent.push_back(m);
+            CHECK(client.SendBinaryAsync(m.data(), m.size()));
+            if (i % 7 == 0)
+                pump();
+        }
+        pump();
+        CHECK(client.messages == sent);
     }
 }
 
