@@ -526,6 +526,35 @@ def echo_c1_leg(seconds=3.0, timeout=120):
     return out
 
 
+def multicast_leg(seconds=2.0, timeout=120):
+    """ws_multicast (performance/ws_multicast_server.cpp:104-124: RATE
+    MulticastBinary calls of 32 zero bytes per tick to every client;
+    ws_multicast_client.cpp:48-51 counts received bytes) through the drop-in
+    WSServer / WSClient over in-memory transports (tools/_build/
+    bench_multicast).  Server frames have key 0, so the XOR is the identity
+    (no GPU pass): this measures the API's framing and fan-out copies.
+    per_call = each call on its own, tick = one BatchScope per tick."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "tools", "_build", "bench_multicast")
+    if not os.path.exists(exe):
+        return None
+    out = {}
+    for leg, args in (("per_call_1c", ["per_call", "1", "1000", "32"]),
+                      ("tick_1c", ["tick", "1", "1000", "32"]),
+                      ("per_call_100c", ["per_call", "100", "1000", "32"]),
+                      ("tick_100c", ["tick", "100", "1000", "32"])):
+        r = subprocess.run([exe] + args + [str(seconds)], capture_output=True, text=True, timeout=timeout)
+        if r.returncode != 0:
+            out[leg] = {"error": (r.stderr or r.stdout).strip()[-300:]}
+            continue
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        out[leg] = {k: d[k] for k in ("msg_per_s", "MiB_per_s", "total_messages", "all_delivered")}
+    out["reference_published"] = {"msg_per_s_1c_1t": 3148135, "msg_per_s_100c_4t": 3225965,
+                                  "hardware": "i7-4790K, loopback sockets (README.md:3542-3580)"}
+    return out
+
+
 def echo_size_leg(w, n=1 << 20, size=32, reps=20):
     """Echo-sized frames on the device batch paths (SURVEY C1's 32 B messages,
     38 B masked client frames): one batch of 1 Mi frames encoded
@@ -822,6 +851,9 @@ def main():
             c1 = echo_c1_leg()
             if c1 is not None:
                 extras["echo_c1"] = c1
+            mc = multicast_leg()
+            if mc is not None:
+                extras["ws_multicast"] = mc
     cpu1 = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu1, cpu_mt = cpu_baseline(w, args.cpu_seconds, host_cpu())
