@@ -284,8 +284,8 @@ bool TLSTransport::Handshake()
         if (_failed)
             return false;
         out = drain_records();
+        return out.empty() || _lower.SendAsync(out.data(), out.size());
     }
-    return out.empty() || _lower.SendAsync(out.data(), out.size());
 }
 
 bool TLSTransport::HandshakeSync()
@@ -362,9 +362,9 @@ bool TLSTransport::Feed(const void* buffer, size_t size, const Plain& plain, con
             }
         }
         out = drain_records();   // handshake replies, session tickets, key updates
+        if (!out.empty())
+            _lower.SendAsync(out.data(), out.size());
     }
-    if (!out.empty())
-        _lower.SendAsync(out.data(), out.size());
     // what the callbacks send (an echo, the upgrade after the handshake)
     // is held back and encrypted once they return: one SSL_write, full
     // records, instead of one record per frame
@@ -372,17 +372,16 @@ bool TLSTransport::Feed(const void* buffer, size_t size, const Plain& plain, con
         handshaked();
     if (!text.empty() && plain)
         plain(text.data(), text.size());
-    std::vector<uint8_t> rec;
     {
         std::lock_guard<std::recursive_mutex> g(_lock);
         if (--_feeding == 0 && !_out_plain.empty()) {
-            std::vector<uint8_t> p;
+            std::vector<uint8_t> p, rec;
             p.swap(_out_plain);
             encrypt(p.data(), p.size(), rec);
+            if (!rec.empty())
+                _lower.SendAsync(rec.data(), rec.size());
         }
     }
-    if (!rec.empty())
-        _lower.SendAsync(rec.data(), rec.size());
     return !_failed;
 }
 
@@ -421,8 +420,12 @@ size_t TLSTransport::encrypt_after_pending(const void* buffer, size_t size, std:
     return n;
 }
 
+// Records go to the lower transport under the session lock: records are
+// sequence-numbered, so two threads' records must reach it in the order
+// they were encrypted.
 size_t TLSTransport::Send(const void* buffer, size_t size)
 {
+    std::lock_guard<std::recursive_mutex> g(_lock);
     std::vector<uint8_t> rec;
     if (encrypt_after_pending(buffer, size, rec) != size)
         return 0;
@@ -431,6 +434,7 @@ size_t TLSTransport::Send(const void* buffer, size_t size)
 
 size_t TLSTransport::Send(const void* buffer, size_t size, const CppCommon::Timespan& timeout)
 {
+    std::lock_guard<std::recursive_mutex> g(_lock);
     std::vector<uint8_t> rec;
     if (encrypt_after_pending(buffer, size, rec) != size)
         return 0;
@@ -439,15 +443,13 @@ size_t TLSTransport::Send(const void* buffer, size_t size, const CppCommon::Time
 
 bool TLSTransport::SendAsync(const void* buffer, size_t size)
 {
-    {
-        std::lock_guard<std::recursive_mutex> g(_lock);
-        if (_failed || !_handshaked)
-            return false;
-        if (_feeding) {   // inside a feed's callbacks: encrypted when they return
-            const uint8_t* p = static_cast<const uint8_t*>(buffer);
-            _out_plain.insert(_out_plain.end(), p, p + size);
-            return true;
-        }
+    std::lock_guard<std::recursive_mutex> g(_lock);
+    if (_failed || !_handshaked)
+        return false;
+    if (_feeding) {   // inside a feed's callbacks: encrypted when they return
+        const uint8_t* p = static_cast<const uint8_t*>(buffer);
+        _out_plain.insert(_out_plain.end(), p, p + size);
+        return true;
     }
     std::vector<uint8_t> rec;
     if (encrypt_after_pending(buffer, size, rec) != size)
@@ -498,16 +500,15 @@ size_t TLSTransport::Receive(void* buffer, size_t size, const CppCommon::Timespa
 
 bool TLSTransport::Disconnect()
 {
-    std::vector<uint8_t> out;
     {
         std::lock_guard<std::recursive_mutex> g(_lock);
         if (_handshaked && !_failed) {
             SSL_shutdown(_ssl);   // close_notify
-            out = drain_records();
+            const std::vector<uint8_t> out = drain_records();
+            if (!out.empty())
+                _lower.Send(out.data(), out.size());
         }
     }
-    if (!out.empty())
-        _lower.Send(out.data(), out.size());
     return _lower.Disconnect();
 }
 

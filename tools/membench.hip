@@ -652,6 +652,16 @@ int main(int argc, char** argv)
                          k_stream<256, 4, 3><<<int(tiles / per), 256>>>(P(s), P(s + bytes), n16, 9u);
                      }));
             }
+            // 512- and 1024-thread blocks, one 32 / 64 KiB tile each (half /
+            // a quarter of the blocks, nothing sequential inside a block)
+            show("512-thread blocks, one 32 KiB tile", time_kernel([&](int i) {
+                     const uint64_t s = (i & 1) * 2 * bytes;
+                     k_stream<512, 4, 3><<<int(tiles / 2), 512>>>(P(s), P(s + bytes), n16, 9u);
+                 }));
+            show("1024-thread blocks, one 64 KiB tile", time_kernel([&](int i) {
+                     const uint64_t s = (i & 1) * 2 * bytes;
+                     k_stream<1024, 4, 3><<<int(tiles / 4), 1024>>>(P(s), P(s + bytes), n16, 9u);
+                 }));
         }
 #undef WAYS
         CK(hipFree(base));
