@@ -706,6 +706,33 @@ static void test_wss()
         }
         pump();
         CHECK(client.messages == sent);
+
+        // four threads sending on the one TLS connection at once (outside
+        // any read): records stay in sequence, every thread's messages
+        // arrive in its own order
+        client.messages.clear();
+        constexpr int T = 4, M = 50;
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&client, t] {
+                for (int m = 0; m < M; ++m) {
+                    const uint8_t msg[3] = {uint8_t(t), uint8_t(m), uint8_t(t ^ m)};
+                    client.SendBinaryAsync(msg, sizeof msg);
+                }
+            });
+        for (auto& x : th)
+            x.join();
+        pump();
+        CHECK(client.messages.size() == size_t(T) * M);
+        int next_of[T] = {0, 0, 0, 0};
+        bool ordered = true;
+        for (const auto& m : client.messages) {
+            if (m.size() != 3 || m[0] >= T || m[1] != next_of[m[0]] || m[2] != uint8_t(m[0] ^ m[1]))
+                ordered = false;
+            else
+                ++next_of[m[0]];
+        }
+        CHECK(ordered);
     }
 }
 
