@@ -27,6 +27,7 @@ struct wsg_ctx {
     int num_cus = 256;
     int blocks_per_cu = 32;       // encode / fan-out / xor grids
     int enc_blocks_per_cu = 1024; // k_encode_mask grid, ~1-2 pieces per wave (tools/tune_enc.py: C5 share -15 %, C3-like -6 % vs 32)
+    uint64_t xor_direct_max = 64 << 10;   // per-call XOR: kernel on the pinned stage up to this size (A/B: $WSG_XOR_DIRECT_MAX)
     int dec_tiles_per_block = 0;   // 0: grid from dec_blocks_per_cu alone; k: ceil(tiles / k) blocks (A/B)
     int dec_blocks_per_cu = 4096;  // k_decode grid cap: one 16 KiB tile per block up to 16 GiB of wire (tools/tune.py, round 2: C2 84.3 vs 85.1 us at 48 blocks/CU, 88.1 at two tiles per block; C3 ragged 0.685 vs 0.705 ms at 256, 0.783 at 48)
     int fan_waves_per_cu = 8;    // fan-out period path: waves per CU (tools/tune_enc.py CFG=c4: 8 best of 4-32)
@@ -268,6 +269,8 @@ int wsg_create(int device, wsg_ctx** out)
         if (v > 0 && v <= 4096)
             c->blocks_per_cu = c->dec_blocks_per_cu = c->enc_blocks_per_cu = v;   // A/B runs: every grid
     }
+    if (const char* e = std::getenv("WSG_XOR_DIRECT_MAX"))   // A/B measurements (per-call path)
+        c->xor_direct_max = std::strtoull(e, nullptr, 10);
     if (const char* e = std::getenv("WSG_DEC_TILES_PER_BLOCK")) {   // A/B measurements (tools/tune.py)
         const int v = std::atoi(e);
         if (v >= 0 && v <= 64)
@@ -591,11 +594,18 @@ int wsg_xor_host(wsg_ctx* c, const void* src, void* dst, size_t len, uint32_t ke
         return rc;
     hipStream_t s = c->stream;
     std::memcpy(c->h_stage, src, len);
-    WSG_HIP(hipMemcpyAsync(c->d_stage, c->h_stage, len, hipMemcpyHostToDevice, s));
     const uint64_t chunks = ceil_div(len, wsg::CHUNK);
-    WSG_HIP(wsg::launch_xor(s, grid_for(c, ceil_div(chunks, wsg::BLOCK)), c->d_stage, c->d_stage, len, key, phase));
-    WSG_HIP(hipMemcpyAsync(c->h_stage, c->d_stage, len, hipMemcpyDeviceToHost, s));
-    WSG_HIP(hipStreamSynchronize(s));
+    if (len <= c->xor_direct_max) {
+        // small payloads (a message of the per-call path): the kernel reads
+        // and writes the page-locked stage itself over PCIe, one launch and
+        // one sync instead of H2D + kernel + D2H
+        WSG_HIP(wsg::launch_xor(s, grid_for(c, ceil_div(chunks, wsg::BLOCK)), c->h_stage, c->h_stage, len, key, phase));
+    } else {
+        WSG_HIP(hipMemcpyAsync(c->d_stage, c->h_stage, len, hipMemcpyHostToDevice, s));
+        WSG_HIP(wsg::launch_xor(s, grid_for(c, ceil_div(chunks, wsg::BLOCK)), c->d_stage, c->d_stage, len, key, phase));
+        WSG_HIP(hipMemcpyAsync(c->h_stage, c->d_stage, len, hipMemcpyDeviceToHost, s));
+    }
+    WSG_HIP(hipStreamSynchronize(s));   // (polling hipStreamQuery instead: same at 1 thread, -9 % at 4)
     std::memcpy(dst, c->h_stage, len);
     return WSG_OK;
 }
