@@ -740,6 +740,29 @@ def c5_job_leg(world, rank, device, codec, n_total=1 << 20, size=16384, chunk=10
     return res
 
 
+def c5_capi_leg(world, rank, n_total=1 << 20, timeout=300):
+    """C5 through the one-process multi-GPU C-ABI entry (SURVEY §8b-3:
+    wsg_mgpu_create over all N GPUs, RCCL inside the library), what a C++
+    server calls: tools/mgpu_c5.py, run by rank 0 in a child process under a
+    time limit while the other ranks wait at a barrier (a collective that
+    fails to start must not hold the bench line)."""
+    import subprocess
+
+    res = None
+    if rank == 0:
+        try:
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mgpu_c5.py"), str(world), str(n_total)],
+                               capture_output=True, text=True, timeout=timeout)
+            if r.returncode == 0:
+                res = json.loads(r.stdout.strip().splitlines()[-1])
+            else:
+                res = {"error": (r.stderr or r.stdout).strip()[-300:]}
+        except subprocess.TimeoutExpired:
+            res = {"error": "no result within %d s" % timeout}
+    barrier(world)
+    return res
+
+
 def fanout_many_leg(w, m=16, reps=10):
     """The multicast tick (ws_multicast_server.cpp:104-114: `messages_rate`
     messages per tick, each to every client) as ONE wsg_fanout_encode_many
@@ -835,6 +858,10 @@ def main():
                                           n_total=int(os.environ.get("WSG_C5_FRAMES", 1 << 20)))
         except Exception as e:   # noqa: BLE001
             extras["c5_job"] = {"error": repr(e)[:300]}
+        if os.environ.get("WSG_BENCH_CAPI_RCCL", "1") != "0":
+            capi = c5_capi_leg(world, rank, n_total=int(os.environ.get("WSG_C5_FRAMES", 1 << 20)))
+            if capi is not None:
+                extras["c5_job_capi"] = capi
     if rank == 0 and world == 1 and not args.no_extras:
         extras["copy_ceiling_GBps"] = round(copy_ceiling(w), 1)
         pc = pcie_inclusive(w)

@@ -1,0 +1,69 @@
+"""C5 through the one-process multi-GPU C-ABI entry (wsg_mgpu_create over
+several GPUs, ncclCommInitAll inside the library): the
+1 Mi x 16 KiB job dealt round-robin in 1024-frame chunks to the GPUs, every
+GPU encodes its shard, wsg_mgpu_encode_gather moves the framed chunks to
+device 0 (grouped ncclSend/ncclRecv); the root checks sampled frames against
+the oracle.  Prints one JSON object.  bench.py runs it from rank 0 at N > 1
+(in its own process, under a time limit).
+
+usage: python tools/mgpu_c5.py NGPUS [n_total] [size] [chunk]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import cppserver_amd as ca  # noqa: E402
+import oracle  # noqa: E402  (the checker)
+from cppserver_amd import shard  # noqa: E402
+from cppserver_amd import workloads as wl  # noqa: E402
+
+
+def main():
+    ngpu = int(sys.argv[1])
+    n_total = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
+    size = int(sys.argv[3]) if len(sys.argv) > 3 else 16384
+    chunk = int(sys.argv[4]) if len(sys.argv) > 4 else 1024
+    devs = list(range(ngpu))
+    g = ca.MultiGPU(devs)
+    try:
+        fsz = ca.frame_size(0x82, True, size)
+        payloads, descs, wires, woffs = [], [], [], []
+        for r in devs:
+            ids = shard.rank_frames(r, ngpu, n_total, chunk)
+            dev = torch.device("cuda", r)
+            payloads.append(wl.c5_payload_torch(ids, size, device=dev))
+            descs.append(ca.desc_to_tensor(wl.c5_desc(ids, size), dev))
+            wires.append(torch.empty(len(ids) * fsz, dtype=torch.uint8, device=dev))
+            woffs.append(torch.empty(len(ids) + 1, dtype=torch.int64, device=dev))
+        out = torch.empty(n_total * fsz, dtype=torch.uint8, device="cuda:0")
+        out_off = torch.empty(n_total + 1, dtype=torch.int64, device="cuda:0")
+        for d in devs:
+            torch.cuda.synchronize(d)
+        g.encode_gather(n_total, chunk, payloads, descs, wires, woffs, root=0, out=out, out_off=out_off)   # warm
+        t0 = time.perf_counter()
+        enc_ms, gat_ms = g.encode_gather(n_total, chunk, payloads, descs, wires, woffs, root=0, out=out,
+                                         out_off=out_off)
+        wall = time.perf_counter() - t0
+        ok = int(out_off[-1].item()) == n_total * fsz
+        for gi in sorted({0, 1, chunk, n_total // 2 + 3, n_total - 1}):
+            ids = np.array([gi])
+            ref, _ = oracle.encode_batch(wl.c5_payload_np(ids, size), wl.c5_desc(ids, size))
+            ok &= bool(np.array_equal(out[gi * fsz: (gi + 1) * fsz].cpu().numpy(), ref))
+        moved = n_total * fsz - int(wires[0].numel())
+        print(json.dumps({"workload": "C5: %d x %d B frames over %d GPUs of one process (wsg_mgpu_create), "
+                                      "gather to device 0 over RCCL" % (n_total, size, ngpu),
+                          "encode_ms": round(enc_ms, 3), "gather_ms": round(gat_ms, 3),
+                          "wall_ms": round(wall * 1e3, 3), "bytes_into_root": moved,
+                          "GBps_into_root": round(moved / (gat_ms * 1e-3) / 1e9, 1) if gat_ms > 0 else None,
+                          "root_check": bool(ok)}))
+    finally:
+        g.close()
+
+
+if __name__ == "__main__":
+    main()
