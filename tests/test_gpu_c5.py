@@ -187,3 +187,19 @@ def test_mgpu_rejects_wrong_shard():
         assert e.value.code == ca.WSG_EINVAL
     finally:
         g.close()
+
+
+@pytest.mark.gpu
+def test_mgpu_c5_tool_world1():
+    """tools/mgpu_c5.py (the C-ABI leg bench.py runs at N > 1) at world 1 on
+    a reduced job: encode + gather through wsg_mgpu_create, root check."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "mgpu_c5.py"), "1", "8192"],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-500:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["root_check"] is True
