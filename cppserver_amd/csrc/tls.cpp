@@ -368,20 +368,26 @@ bool TLSTransport::Feed(const void* buffer, size_t size, const Plain& plain, con
     // what the callbacks send (an echo, the upgrade after the handshake)
     // is held back and encrypted once they return: one SSL_write, full
     // records, instead of one record per frame
+    // the held-back bytes go out when the callbacks return, also when one
+    // of them throws (the exception then continues to the caller)
+    struct Release {
+        TLSTransport* t;
+        ~Release()
+        {
+            std::lock_guard<std::recursive_mutex> g(t->_lock);
+            if (--t->_feeding == 0 && !t->_out_plain.empty()) {
+                std::vector<uint8_t> p, rec;
+                p.swap(t->_out_plain);
+                t->encrypt(p.data(), p.size(), rec);
+                if (!rec.empty())
+                    t->_lower.SendAsync(rec.data(), rec.size());
+            }
+        }
+    } release{this};
     if (just_handshaked && handshaked)
         handshaked();
     if (!text.empty() && plain)
         plain(text.data(), text.size());
-    {
-        std::lock_guard<std::recursive_mutex> g(_lock);
-        if (--_feeding == 0 && !_out_plain.empty()) {
-            std::vector<uint8_t> p, rec;
-            p.swap(_out_plain);
-            encrypt(p.data(), p.size(), rec);
-            if (!rec.empty())
-                _lower.SendAsync(rec.data(), rec.size());
-        }
-    }
     return !_failed;
 }
 
