@@ -7,7 +7,9 @@
  * frame to the transport.  The timeout overloads (CppCommon::Timespan,
  * server/ws/ws_common.h) pass the timeout to the transport's Send / Receive.
  * Connect(resolver) / ConnectAsync(resolver) take an Asio resolver in the
- * reference; name resolution belongs to the transport here.
+ * reference (ws_client.h:40-42); name resolution belongs to the transport
+ * here, so these overloads accept any resolver handle and connect as
+ * Connect() / ConnectAsync() do (the transport is already connected).
  */
 #ifndef CPPSERVER_AMD_WS_CLIENT_H
 #define CPPSERVER_AMD_WS_CLIENT_H
@@ -33,6 +35,12 @@ public:
     //! As Connect, with the upgrade request queued on the transport
     //! (reference ws_client.cpp:22-30: HTTPClient::ConnectAsync, then onConnected)
     virtual bool ConnectAsync();
+    //! Reference signatures with a resolver (ws_client.h:40-42); the
+    //! transport resolved and connected already
+    template <class Resolver>
+    bool Connect(const std::shared_ptr<Resolver>&) { return Connect(); }
+    template <class Resolver>
+    bool ConnectAsync(const std::shared_ptr<Resolver>&) { return ConnectAsync(); }
     virtual bool Disconnect();
     bool IsConnected() const { return _transport.IsConnected() && _ws_handshaked; }
 

@@ -103,6 +103,14 @@ public:
 
 [[maybe_unused]] void use_wss(WSSClient& c, WSSServer& s) { (void)c.SendTextAsync("tls"); (void)s.MulticastText("tls"); }
 
+// Connect / ConnectAsync with a resolver, as ws_chat_client.cpp calls them
+struct TCPResolver {};
+[[maybe_unused]] void use_resolver(ChatClient& c, const std::shared_ptr<TCPResolver>& resolver)
+{
+    (void)c.Connect(resolver);
+    (void)c.ConnectAsync(resolver);
+}
+
 // the reference's SSL context set-up, verbatim in form
 // (examples/wss_chat_server.cpp:98-102, examples/wss_chat_client.cpp:105-109)
 [[maybe_unused]] std::shared_ptr<CppServer::Asio::SSLContext> server_context()
