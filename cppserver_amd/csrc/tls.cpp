@@ -4,6 +4,7 @@
 // include/server/asio/ssl_*.h).  Host control plane; no GPU code.
 #include "server/asio/ssl_context.h"
 #include "server/ws/tls_transport.h"
+#include "server/ws/ws_batch.h"
 
 #include <openssl/bio.h>
 #include <openssl/err.h>
@@ -233,8 +234,23 @@ TLSTransport::TLSTransport(std::shared_ptr<Asio::SSLContext> context, Transport&
 
 TLSTransport::~TLSTransport()
 {
+    BatchScope::Cancel(this);
     if (_ssl)
         SSL_free(_ssl);
+}
+
+void TLSTransport::scope_end(void* self)
+{
+    auto* t = static_cast<TLSTransport*>(self);
+    std::lock_guard<std::recursive_mutex> g(t->_lock);
+    t->_scope_held = false;
+    if (t->_out_plain.empty() || t->_feeding)
+        return;
+    std::vector<uint8_t> p, rec;
+    p.swap(t->_out_plain);
+    t->encrypt(p.data(), p.size(), rec);
+    if (!rec.empty())
+        t->_lower.SendAsync(rec.data(), rec.size());
 }
 
 bool TLSTransport::fail(const char* what)
@@ -455,6 +471,15 @@ bool TLSTransport::SendAsync(const void* buffer, size_t size)
     if (_feeding) {   // inside a feed's callbacks: encrypted when they return
         const uint8_t* p = static_cast<const uint8_t*>(buffer);
         _out_plain.insert(_out_plain.end(), p, p + size);
+        return true;
+    }
+    if (BatchScope::Active()) {   // inside a batch scope (an event-loop tick): encrypted when it ends
+        const uint8_t* p = static_cast<const uint8_t*>(buffer);
+        _out_plain.insert(_out_plain.end(), p, p + size);
+        if (!_scope_held) {
+            _scope_held = true;
+            BatchScope::AtEnd(this, &TLSTransport::scope_end);
+        }
         return true;
     }
     std::vector<uint8_t> rec;

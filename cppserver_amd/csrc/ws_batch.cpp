@@ -13,8 +13,10 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <stdexcept>
+#include <thread>
 #include <string>
 
 namespace CppServer {
@@ -475,6 +477,36 @@ AutoState& auto_state()
     return st;
 }
 
+// AtEnd registrations: (thread, key, fn), process-wide so that Cancel works
+// from any thread
+struct EndHook {
+    std::thread::id thread;
+    void* key;
+    void (*fn)(void*);
+};
+std::mutex g_end_lock;
+std::vector<EndHook> g_end_hooks;
+
+void run_end_hooks()
+{
+    std::vector<EndHook> mine;
+    {
+        std::lock_guard<std::mutex> g(g_end_lock);
+        const auto me = std::this_thread::get_id();
+        for (size_t i = 0; i < g_end_hooks.size();) {
+            if (g_end_hooks[i].thread == me) {
+                mine.push_back(g_end_hooks[i]);
+                g_end_hooks[i] = g_end_hooks.back();
+                g_end_hooks.pop_back();
+            } else {
+                ++i;
+            }
+        }
+    }
+    for (const EndHook& h : mine)
+        h.fn(h.key);
+}
+
 } // namespace
 
 BatchScope::BatchScope() noexcept { ++auto_state().depth; }
@@ -485,11 +517,35 @@ BatchScope::~BatchScope()
     if (st.depth == 1 && !st.draining) {
         try {
             Flush();
+            run_end_hooks();
         } catch (...) {
             // a destructor must not throw; the frames stay queued for the next flush
         }
     }
     --st.depth;
+}
+
+void BatchScope::AtEnd(void* key, void (*fn)(void*))
+{
+    std::lock_guard<std::mutex> g(g_end_lock);
+    const auto me = std::this_thread::get_id();
+    for (const EndHook& h : g_end_hooks)
+        if (h.key == key && h.thread == me)
+            return;
+    g_end_hooks.push_back(EndHook{me, key, fn});
+}
+
+void BatchScope::Cancel(void* key)
+{
+    std::lock_guard<std::mutex> g(g_end_lock);
+    for (size_t i = 0; i < g_end_hooks.size();) {
+        if (g_end_hooks[i].key == key) {
+            g_end_hooks[i] = g_end_hooks.back();
+            g_end_hooks.pop_back();
+        } else {
+            ++i;
+        }
+    }
 }
 
 size_t BatchScope::Flush()

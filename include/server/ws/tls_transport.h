@@ -15,7 +15,9 @@
  *    lower.SendAsync (one call per Send, after SSL_write).  SendAsync calls
  *    made from inside Feed's callbacks (an echo, a batch flush at the end
  *    of a read) are held back and encrypted together when the callbacks
- *    return: full 16 KiB records instead of one record per frame.
+ *    return: full 16 KiB records instead of one record per frame; likewise
+ *    SendAsync inside a BatchScope (an event-loop tick, ws_batch.h) is
+ *    encrypted when the outermost scope on that thread ends.
  *  - Feed: records read from `lower` (what its owner's onReceived gets);
  *    advances the handshake, hands decrypted bytes to `plain` and calls
  *    `handshaked` once when the handshake completes.
@@ -95,8 +97,9 @@ private:
     std::string _error;
     std::vector<uint8_t> _pending;   // plaintext decrypted by Receive beyond what was asked
     size_t _pending_at{0};
-    std::vector<uint8_t> _out_plain;   // SendAsync bytes held back while a Feed runs its callbacks
+    std::vector<uint8_t> _out_plain;   // SendAsync bytes held back while a Feed runs its callbacks / a batch scope is open
     int _feeding{0};
+    bool _scope_held{false};           // registered to flush _out_plain when this thread's batch scope ends
     mutable std::recursive_mutex _lock;
 
     // encrypted bytes waiting in _wbio (handshake records, application records)
@@ -106,6 +109,7 @@ private:
     bool fail(const char* what);
     size_t encrypt(const void* buffer, size_t size, std::vector<uint8_t>& records);
     size_t encrypt_after_pending(const void* buffer, size_t size, std::vector<uint8_t>& records);
+    static void scope_end(void* self);
 };
 
 } // namespace WS

@@ -232,6 +232,13 @@ public:
     static WSSendBatch& Send();
     //! Early flush when a batch passed the limits (inside a scope)
     static void CheckLimits();
+
+    //! Call fn(key) once when the outermost scope on this thread ends, after
+    //! its last flush (a transport that coalesces what one scope sends: the
+    //! TLS records of a tick).  Registering a key twice is one call;
+    //! Cancel(key) drops it (the object is going away).
+    static void AtEnd(void* key, void (*fn)(void*));
+    static void Cancel(void* key);
 };
 
 } // namespace WS
