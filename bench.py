@@ -511,7 +511,8 @@ def echo_c1_leg(seconds=3.0, timeout=120):
             # wss_echo (performance/wss_echo_client.cpp): the same loop through
             # WSSClient / WSSSession over TLS 1.3 (OpenSSL record encryption)
             ("wss_per_read_1c", ["per_read", "1", "1", "1000", "32"]),
-            ("wss_per_read_100c_4t", ["per_read", "100", "4", "1000", "32"]))
+            ("wss_per_read_100c_4t", ["per_read", "100", "4", "1000", "32"]),
+            ("wss_tick_100c_1t", ["tick", "100", "1", "1000", "32"]))
     for leg, args in legs:
         extra = ["tls"] if leg.startswith("wss_") else []
         r = subprocess.run([exe] + args + [str(seconds)] + extra, capture_output=True, text=True, timeout=timeout)
