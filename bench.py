@@ -65,6 +65,10 @@ def dist_setup(args):
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # a host-side group for waits that must not park an RCCL kernel on
+            # the GPUs (c5_capi_leg: a child process drives every GPU meanwhile)
+            global CPU_GROUP
+            CPU_GROUP = dist.new_group(backend="gloo")
         else:
             dist.init_process_group(backend)
     else:
@@ -72,11 +76,14 @@ def dist_setup(args):
     return rank, world, local
 
 
-def barrier(world):
+CPU_GROUP = None
+
+
+def barrier(world, group=None):
     if world > 1:
         import torch.distributed as dist
 
-        dist.barrier()
+        dist.barrier(group=group)
 
 
 def max_over_ranks(x, world, device):
@@ -760,7 +767,7 @@ def c5_capi_leg(world, rank, n_total=1 << 20, timeout=300):
                 res = {"error": (r.stderr or r.stdout).strip()[-300:]}
         except subprocess.TimeoutExpired:
             res = {"error": "no result within %d s" % timeout}
-    barrier(world)
+    barrier(world, CPU_GROUP)
     return res
 
 
