@@ -345,9 +345,9 @@ bool TLSTransport::Feed(const void* buffer, size_t size, const Plain& plain, con
     bool just_handshaked = false;
     {
         std::lock_guard<std::recursive_mutex> g(_lock);
-        ++_feeding;
         if (_failed)
             return false;
+        ++_feeding;
         if (size && BIO_write(_rbio, buffer, int(size)) != int(size)) {
             --_feeding;
             return fail("BIO_write");
