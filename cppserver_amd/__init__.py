@@ -98,6 +98,10 @@ def lib(path=None):
         "wsg_mgpu_ctx": (vp, [vp, ci]),
         "wsg_mgpu_shard_count": (u64, [u64, u32, ci, ci]),
         "wsg_mgpu_encode_gather": (ci, [vp, u64, u32, vp, vp, vp, vp, vp, vp, ci, vp, u64, vp, vp]),
+        "wsg_decode_batch_host_multi": (ci, [vp, ci, vp, u64, vp, u32, vp, vp]),
+        "wsg_encode_batch_host_multi": (ci, [vp, ci, vp, u64, vp, u32, vp, u64, vp]),
+        "wsg_mgpu_decode_batch_host": (ci, [vp, vp, u64, vp, u32, vp, vp]),
+        "wsg_mgpu_encode_batch_host": (ci, [vp, vp, u64, vp, u32, vp, u64, vp]),
         "wsg_timing_enable": (ci, [vp, ci]),
         "wsg_timing_read": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ci]),
     }
@@ -504,6 +508,47 @@ def _ptr_array(ptrs):
     return (ctypes.c_void_p * len(ptrs))(*[ctypes.c_void_p(p) for p in ptrs])
 
 
+def _host_decode_args(wire, frame_start, out):
+    wire = np.ascontiguousarray(wire, dtype=np.uint8)
+    fs = np.ascontiguousarray(frame_start, dtype=np.uint64)
+    if out is None:
+        out = np.empty(max(len(wire), 1), dtype=np.uint8)
+    info = np.zeros(max(len(fs), 1), dtype=RECV_INFO)
+    return wire, fs, out, info
+
+
+def _host_encode_args(payload, desc, wire):
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    desc = np.ascontiguousarray(desc, dtype=SEND_DESC)
+    total = int(frame_sizes(desc).sum()) if len(desc) else 0
+    if wire is None:
+        wire = np.empty(max(total, 1), dtype=np.uint8)
+    off = np.zeros(len(desc) + 1, dtype=np.uint64)
+    return payload, desc, wire, off, total
+
+
+def decode_batch_host_multi(codecs, wire, frame_start, out=None):
+    """wsg_decode_batch_host_multi: one host batch over several contexts
+    (their GPUs' PCIe links at once).  Returns (rc, out, info) like
+    Codec.decode_batch_host."""
+    wire, fs, out, info = _host_decode_args(wire, frame_start, out)
+    ctxs = _ptr_array([c._ctx.value for c in codecs])
+    rc = lib().wsg_decode_batch_host_multi(ctxs, len(codecs), _np_ptr(wire), len(wire), _np_ptr(fs), len(fs),
+                                           _np_ptr(out), _np_ptr(info))
+    return rc, out[: len(wire)], info[: len(fs)]
+
+
+def encode_batch_host_multi(codecs, payload, desc, wire=None):
+    """wsg_encode_batch_host_multi: returns (rc, wire bytes, wire_off)."""
+    payload, desc, wire, off, total = _host_encode_args(payload, desc, wire)
+    ctxs = _ptr_array([c._ctx.value for c in codecs])
+    n = len(desc)
+    rc = lib().wsg_encode_batch_host_multi(ctxs, len(codecs), _np_ptr(payload) if len(payload) else None,
+                                           len(payload), _np_ptr(desc) if n else None, n, _np_ptr(wire), len(wire),
+                                           _np_ptr(off))
+    return rc, wire[:total], off
+
+
 class MultiGPU:
     """The multi-GPU entry of the C-ABI (wsg_mgpu_*): round-robin shards of a
     frame batch encoded on their GPUs and gathered to one rank over RCCL.
@@ -568,4 +613,19 @@ class MultiGPU:
             ctypes.c_void_p(out_off.data_ptr() if out_off is not None else 0), times)
         _check(rc, "wsg_mgpu_encode_gather")
         return times[0], times[1]
+
+    def decode_batch_host(self, wire, frame_start, out=None):
+        """wsg_mgpu_decode_batch_host: a host batch over this process's GPUs."""
+        wire, fs, out, info = _host_decode_args(wire, frame_start, out)
+        rc = self._L.wsg_mgpu_decode_batch_host(self._g, _np_ptr(wire), len(wire), _np_ptr(fs), len(fs),
+                                                _np_ptr(out), _np_ptr(info))
+        return rc, out[: len(wire)], info[: len(fs)]
+
+    def encode_batch_host(self, payload, desc, wire=None):
+        payload, desc, wire, off, total = _host_encode_args(payload, desc, wire)
+        n = len(desc)
+        rc = self._L.wsg_mgpu_encode_batch_host(self._g, _np_ptr(payload) if len(payload) else None, len(payload),
+                                                _np_ptr(desc) if n else None, n, _np_ptr(wire), len(wire),
+                                                _np_ptr(off))
+        return rc, wire[:total], off
 

@@ -218,6 +218,8 @@ int drain_timing(wsg_ctx* c)
 
 } // namespace
 
+int wsg::ctx_device(const wsg_ctx* c) { return c ? c->device : 0; }
+
 extern "C" {
 
 int wsg_abi_version(void) { return WSG_ABI_VERSION; }

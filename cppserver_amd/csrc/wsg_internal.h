@@ -89,4 +89,7 @@ hipError_t launch_xor(hipStream_t s, int grid, const uint8_t* src, uint8_t* dst,
 hipError_t launch_rebase_offsets(hipStream_t s, const uint64_t* stage, const uint64_t* goff, uint64_t n_total,
                                  uint32_t chunk, uint64_t* out_off, uint64_t total);
 
+// HIP device a context is bound to (wsg_capi.hip)
+int ctx_device(const wsg_ctx* c);
+
 } // namespace wsg

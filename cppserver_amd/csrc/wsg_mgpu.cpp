@@ -34,6 +34,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -141,12 +142,90 @@ int grow(T*& p, uint64_t& cap, uint64_t want)
     return WSG_OK;
 }
 
+// Runs of a host batch split over `parts` contexts: run k is frames
+// [cut[k], cut[k + 1]), about wire_len / parts wire bytes each, cut at frame
+// starts.  Every cut is a frame starting inside the wire (frames starting at
+// or past its end stay with the last run) and run 0 holds frame 0, so run k
+// covers wire bytes [k ? fs[cut[k]] : 0, cut[k + 1] < n ? fs[cut[k + 1]] : wire_len).
+std::vector<uint32_t> host_runs(const uint64_t* fs, uint32_t n, uint64_t wire_len, int parts)
+{
+    std::vector<uint32_t> cut(size_t(parts) + 1, n);
+    cut[0] = 0;
+    const uint32_t inside = uint32_t(std::lower_bound(fs, fs + n, wire_len) - fs);
+    for (int k = 1; k < parts; ++k) {
+        const uint64_t target = uint64_t(double(wire_len) * k / parts);
+        uint32_t idx = uint32_t(std::lower_bound(fs, fs + inside, target) - fs);
+        idx = std::max<uint32_t>(idx, 1);
+        if (idx >= inside)
+            idx = n;   // no frame starts inside the wire past the target
+        cut[size_t(k)] = std::max(idx, cut[size_t(k) - 1]);
+    }
+    return cut;
+}
+
+// Run fn(i) for i in [0, parts) on threads of their own (i = 0 on the
+// caller's), each with ctxs[i]'s device current.
+template <class Fn>
+void on_contexts(wsg_ctx* const* ctxs, int parts, Fn fn)
+{
+    std::vector<std::thread> th;
+    for (int i = 1; i < parts; ++i)
+        th.emplace_back([&, i] {
+            (void)hipSetDevice(wsg::ctx_device(ctxs[i]));
+            fn(i);
+        });
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(wsg::ctx_device(ctxs[0]));
+    fn(0);
+    (void)hipSetDevice(prev);
+    for (auto& t : th)
+        t.join();
+}
+
+// The contexts a split uses: the first of each device.  Two pipelines on
+// one GPU share its PCIe link and copy engines and measured slower than one
+// (C2 from pinned memory: 29-40 GiB/s on one context, 15-20 on two or four of
+// one device, tools/host_multi.py); $WSG_HOST_MULTI_SHARE=1 keeps every
+// context (the one-GPU tests exercise the split that way).
+std::vector<wsg_ctx*> one_per_device(wsg_ctx* const* ctxs, int nctx)
+{
+    const char* e = std::getenv("WSG_HOST_MULTI_SHARE");
+    const bool share = e && *e == '1';
+    std::vector<wsg_ctx*> v;
+    std::vector<int> seen;
+    for (int i = 0; i < nctx; ++i) {
+        const int d = wsg::ctx_device(ctxs[i]);
+        if (!share && std::find(seen.begin(), seen.end(), d) != seen.end())
+            continue;
+        seen.push_back(d);
+        v.push_back(ctxs[i]);
+    }
+    return v;
+}
+
+// A per-run status that is not about the frames (HIP, memory) wins; the
+// frames' own errors are recomputed over the whole batch.
+inline bool frame_status(int rc) { return rc == WSG_OK || rc == WSG_EINVAL || rc == WSG_ETRUNC; }
+
 } // namespace
 
 struct wsg_mgpu {
     int world = 0;
     std::vector<Local> local;   // ranks driven by this process
 };
+
+namespace {
+
+std::vector<wsg_ctx*> local_ctxs(wsg_mgpu* g)
+{
+    std::vector<wsg_ctx*> v;
+    for (Local& l : g->local)
+        v.push_back(l.ctx);
+    return v;
+}
+
+} // namespace
 
 extern "C" {
 
@@ -483,6 +562,127 @@ int wsg_mgpu_encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const 
         times[1] = gat;
     }
     return WSG_OK;
+}
+
+int wsg_decode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* wire, uint64_t wire_len,
+                                const uint64_t* frame_start, uint32_t n, uint8_t* out, wsg_recv_info* info)
+{
+    if (!ctxs || nctx <= 0 || (wire_len && (!wire || !out)) || (n && (!frame_start || !info)))
+        return WSG_EINVAL;
+    for (int i = 0; i < nctx; ++i)
+        if (!ctxs[i])
+            return WSG_EINVAL;
+    const std::vector<wsg_ctx*> use = one_per_device(ctxs, nctx);
+    ctxs = use.data();
+    nctx = int(use.size());
+    bool sorted = true;
+    for (uint32_t i = 1; i < n && sorted; ++i)
+        sorted = frame_start[i] > frame_start[i - 1];
+    const int parts = int(std::min<uint64_t>(uint64_t(nctx), std::max<uint64_t>(n, 1)));
+    if (parts == 1 || !sorted)
+        return wsg_decode_batch_host(ctxs[0], wire, wire_len, frame_start, n, out, info);
+
+    const std::vector<uint32_t> cut = host_runs(frame_start, n, wire_len, parts);
+    std::vector<int> rc(size_t(parts), WSG_OK);
+    on_contexts(ctxs, parts, [&](int k) {
+        const uint32_t a = cut[size_t(k)], b = cut[size_t(k) + 1];
+        if (a == b)
+            return;
+        const uint64_t lo = a ? frame_start[a] : 0, hi = b < n ? frame_start[b] : wire_len;
+        std::vector<uint64_t> fs(frame_start + a, frame_start + b);
+        for (uint64_t& x : fs)
+            x -= lo;
+        rc[size_t(k)] = wsg_decode_batch_host(ctxs[k], wire + lo, hi - lo, fs.data(), b - a, out + lo, info + a);
+        if (lo)
+            for (uint32_t i = a; i < b; ++i)
+                info[i].payload_off += lo;
+    });
+    for (int r : rc)
+        if (!frame_status(r))
+            return r;
+    // the batch's frame errors as the one-context call states them: a frame
+    // that runs into the next one overlaps it (EINVAL) when its whole length
+    // lies inside the wire (a run's last frame only saw its run's bytes)
+    int first = WSG_OK;
+    for (uint32_t i = 0; i < n; ++i) {
+        wsg_recv_info& r = info[i];
+        if (r.error == WSG_ETRUNC && i + 1 < n && frame_start[i] < wire_len) {
+            wsg_recv_info h;
+            if (wsg_header_unpack(wire + frame_start[i], wire_len - frame_start[i], &h) == WSG_OK &&
+                h.len <= wire_len - frame_start[i] - h.hdr_len)
+                r.error = int8_t(WSG_EINVAL);
+        }
+        if (r.error && !first)
+            first = r.error;
+    }
+    return first;
+}
+
+int wsg_encode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* payload, uint64_t payload_len,
+                                const wsg_send_desc* desc, uint32_t n, uint8_t* wire, uint64_t wire_cap,
+                                uint64_t* wire_off)
+{
+    if (!ctxs || nctx <= 0 || !wire_off || (n && (!desc || !wire)) || (payload_len && !payload))
+        return WSG_EINVAL;
+    for (int i = 0; i < nctx; ++i)
+        if (!ctxs[i])
+            return WSG_EINVAL;
+    const std::vector<wsg_ctx*> use = one_per_device(ctxs, nctx);
+    ctxs = use.data();
+    nctx = int(use.size());
+    const int parts = int(std::min<uint64_t>(uint64_t(nctx), std::max<uint64_t>(n, 1)));
+    if (parts == 1)
+        return wsg_encode_batch_host(ctxs[0], payload, payload_len, desc, n, wire, wire_cap, wire_off);
+    // frame offsets (and argument checks) as the one-context call makes them
+    wire_off[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const wsg_send_desc& d = desc[i];
+        if (d.len > payload_len || d.src_off > payload_len - d.len)
+            return WSG_EINVAL;
+        wire_off[i + 1] = wire_off[i] + wsg_frame_size(d.opcode, d.mask, d.len, d.status);
+    }
+    if (wire_off[n] > wire_cap)
+        return WSG_ENOMEM;
+    // runs of about equal wire bytes
+    std::vector<uint32_t> cut(size_t(parts) + 1, n);
+    cut[0] = 0;
+    for (int k = 1; k < parts; ++k) {
+        const uint64_t target = uint64_t(double(wire_off[n]) * k / parts);
+        const uint32_t idx = uint32_t(std::lower_bound(wire_off, wire_off + n, target) - wire_off);
+        cut[size_t(k)] = std::max(std::min(idx, n), cut[size_t(k) - 1]);
+    }
+    std::vector<int> rc(size_t(parts), WSG_OK);
+    on_contexts(ctxs, parts, [&](int k) {
+        const uint32_t a = cut[size_t(k)], b = cut[size_t(k) + 1];
+        if (a == b)
+            return;
+        std::vector<uint64_t> off(size_t(b - a) + 1);
+        rc[size_t(k)] = wsg_encode_batch_host(ctxs[k], payload, payload_len, desc + a, b - a, wire + wire_off[a],
+                                              wire_off[b] - wire_off[a], off.data());
+    });
+    for (int r : rc)
+        if (r)
+            return r;
+    return WSG_OK;
+}
+
+int wsg_mgpu_decode_batch_host(wsg_mgpu* g, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start,
+                               uint32_t n, uint8_t* out, wsg_recv_info* info)
+{
+    if (!g || g->local.empty())
+        return WSG_EINVAL;
+    const std::vector<wsg_ctx*> v = local_ctxs(g);
+    return wsg_decode_batch_host_multi(v.data(), int(v.size()), wire, wire_len, frame_start, n, out, info);
+}
+
+int wsg_mgpu_encode_batch_host(wsg_mgpu* g, const uint8_t* payload, uint64_t payload_len, const wsg_send_desc* desc,
+                               uint32_t n, uint8_t* wire, uint64_t wire_cap, uint64_t* wire_off)
+{
+    if (!g || g->local.empty())
+        return WSG_EINVAL;
+    const std::vector<wsg_ctx*> v = local_ctxs(g);
+    return wsg_encode_batch_host_multi(v.data(), int(v.size()), payload, payload_len, desc, n, wire, wire_cap,
+                                       wire_off);
 }
 
 } // extern "C"

@@ -287,6 +287,30 @@ int wsg_mgpu_encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const 
                            const uint64_t* wire_cap, uint64_t* const* d_wire_off, int root, uint8_t* d_out,
                            uint64_t out_cap, uint64_t* d_out_off, double* times);
 
+/* ---- host batches over several GPUs (one process, no collective) -------- */
+/* The host-staged path is PCIe-bound (one x16 link per GPU): a server whose
+ * receive/send buffers live in host memory (asio socket buffers) spreads one
+ * batch over its GPUs' links.  The frames are cut into contiguous runs
+ * of about equal wire bytes; run i goes through ctxs[i]'s host pipeline
+ * (wsg_decode_batch_host / wsg_encode_batch_host) on a thread of its own,
+ * all runs at once.  Results and status are those of the one-context call
+ * on the whole batch (a frame table that is not strictly increasing takes
+ * that call on ctxs[0]).  Each context is used by this call alone meanwhile.
+ * Only the first context of each device takes a run: two pipelines on one
+ * GPU share its link and copy engines and run slower than one
+ * ($WSG_HOST_MULTI_SHARE=1 splits over every context given).               */
+int wsg_decode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* wire, uint64_t wire_len,
+                                const uint64_t* frame_start, uint32_t n, uint8_t* out, wsg_recv_info* info);
+int wsg_encode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* payload, uint64_t payload_len,
+                                const wsg_send_desc* desc, uint32_t n, uint8_t* wire, uint64_t wire_cap,
+                                uint64_t* wire_off);
+/* The same over the GPUs a wsg_mgpu group drives in this process (its local
+ * ranks' contexts).                                                          */
+int wsg_mgpu_decode_batch_host(wsg_mgpu* g, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start,
+                               uint32_t n, uint8_t* out, wsg_recv_info* info);
+int wsg_mgpu_encode_batch_host(wsg_mgpu* g, const uint8_t* payload, uint64_t payload_len, const wsg_send_desc* desc,
+                               uint32_t n, uint8_t* wire, uint64_t wire_cap, uint64_t* wire_off);
+
 /* ---- kernel timing (measurement hook used by bench.py) ------------------ */
 /* on = k > 0: the ctx records HIP events around the dominant payload kernel of
  * every k-th batch call, on the stream it is launched on (k > 1 keeps the

@@ -203,3 +203,4 @@ def test_mgpu_c5_tool_world1():
     assert r.returncode == 0, r.stderr[-500:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["root_check"] is True
+    assert d["host_decode"].get("check") is True, d["host_decode"]

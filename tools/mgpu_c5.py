@@ -23,6 +23,38 @@ from cppserver_amd import shard  # noqa: E402
 from cppserver_amd import workloads as wl  # noqa: E402
 
 
+def host_leg(g, ngpu, reps=3):
+    """The PCIe-inclusive decode (host wire in pinned memory -> GPUs -> host)
+    of ngpu x 4096 x 64 KiB frames: on device 0 alone, then split over every
+    GPU of the group (wsg_mgpu_decode_batch_host: a run per GPU, each on its
+    own link); payload GiB/s, sampled frames checked against the oracle."""
+    n, size = 4096 * ngpu, 65536
+    wire, fs, _ = wl.c2_wire(n, size, seed=5)
+    pin_in, pin_out = ca.pinned_empty(len(wire)), ca.pinned_empty(len(wire))
+    pin_in[:] = wire
+    del wire
+    one = ca.Codec(0)
+    res = {"workload": "%d x %d B masked frames, pinned host buffers" % (n, size)}
+    try:
+        for name, fn in (("one_gpu", lambda: ca.decode_batch_host_multi([one], pin_in, fs, out=pin_out)),
+                         ("all_gpus", lambda: g.decode_batch_host(pin_in, fs, out=pin_out))):
+            rc, _, _ = fn()
+            assert rc == 0, rc
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            res[name + "_GiBps"] = round(n * size * reps / (time.perf_counter() - t0) / 2**30, 2)
+        ok = True
+        for i in (0, n // 2, n - 1):
+            a, b = int(fs[i]), int(fs[i]) + size + 14
+            rc, ref, _ = oracle.decode_batch(np.array(pin_in[a:b]), np.zeros(1, np.uint64))
+            ok &= rc == 0 and bool(np.array_equal(pin_out[a:b], ref))
+        res["check"] = bool(ok)
+    finally:
+        one.close()
+    return res
+
+
 def main():
     ngpu = int(sys.argv[1])
     n_total = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
@@ -55,12 +87,18 @@ def main():
             ref, _ = oracle.encode_batch(wl.c5_payload_np(ids, size), wl.c5_desc(ids, size))
             ok &= bool(np.array_equal(out[gi * fsz: (gi + 1) * fsz].cpu().numpy(), ref))
         moved = n_total * fsz - int(wires[0].numel())
+        del payloads, wires, out
+        torch.cuda.empty_cache()
+        try:
+            host = host_leg(g, ngpu)
+        except Exception as e:   # noqa: BLE001  (reported, the C5 result stands)
+            host = {"error": repr(e)[:300]}
         print(json.dumps({"workload": "C5: %d x %d B frames over %d GPUs of one process (wsg_mgpu_create), "
                                       "gather to device 0 over RCCL" % (n_total, size, ngpu),
                           "encode_ms": round(enc_ms, 3), "gather_ms": round(gat_ms, 3),
                           "wall_ms": round(wall * 1e3, 3), "bytes_into_root": moved,
                           "GBps_into_root": round(moved / (gat_ms * 1e-3) / 1e9, 1) if gat_ms > 0 else None,
-                          "root_check": bool(ok)}))
+                          "root_check": bool(ok), "host_decode": host}))
     finally:
         g.close()
 
