@@ -470,6 +470,36 @@ __global__ __launch_bounds__(64 * WPB) void k_glds(const uint8_t* __restrict__ s
     }
 }
 
+// Tail shaping: blocks [0, nbig) copy 16 KiB tiles in order, the blocks
+// after them copy the rest in tiles of 256 x 16 x SU bytes, so the last
+// blocks dispatched are short and the launch drains sooner.
+template <int SU, bool REV = false>
+__global__ __launch_bounds__(256) void k_tail(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t nbig,
+                                              uint32_t key)
+{
+    uint64_t base;
+    int units;
+    // REV (control): the short tiles first, the 16 KiB tiles last
+    const uint64_t nsmall = uint64_t(gridDim.x) - nbig;
+    const uint64_t b = REV ? (blockIdx.x < nsmall ? nbig + blockIdx.x : blockIdx.x - nsmall) : blockIdx.x;
+    if (b < nbig) {
+        base = b * 1024;
+        units = 4;
+    } else {
+        base = nbig * 1024 + (b - nbig) * 256 * SU;
+        units = SU;
+    }
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (u < units)
+            v[u] = __builtin_nontemporal_load(src + base + uint64_t(u) * 256 + threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (u < units)
+            __builtin_nontemporal_store(v[u] ^ key, dst + base + uint64_t(u) * 256 + threadIdx.x);
+}
+
 template <class F>
 double time_kernel(F launch, int reps = 20)
 {
@@ -623,6 +653,36 @@ int main(int argc, char** argv)
         }
 #undef WP
         CK(hipFree(d));
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "tail") {
+        // the last pct % of the bytes in short tiles (4 or 8 KiB) vs all 16 KiB
+        // tiles; two buffer pairs in turn, interleaved settings, 3 rounds
+        const uint64_t span = 4 * bytes;
+        uint8_t* base;
+        CK(hipMalloc(&base, span));
+        CK(hipMemset(base, 5, span));
+        auto P = [&](uint64_t off) { return (u32x4*)(base + off); };
+        const uint64_t tiles = n16 / 1024;
+        for (int rep = 0; rep < 3; ++rep)
+            for (int su : {1, 2, -1})
+                for (int pct : {0, 15, 25, 35, 50, 100}) {
+                    const uint64_t nbig = tiles - tiles * pct / 100;
+                    const uint64_t nsmall = (tiles - nbig) * 4 / (su < 0 ? 1 : su);
+                    const int grid = int(nbig + nsmall);
+                    double ms = time_kernel([&](int i) {
+                        const uint64_t s = (i & 1) * 2 * bytes;
+                        if (su == 1)
+                            k_tail<1><<<grid, 256>>>(P(s), P(s + bytes), nbig, 9u);
+                        else if (su == 2)
+                            k_tail<2><<<grid, 256>>>(P(s), P(s + bytes), nbig, 9u);
+                        else
+                            k_tail<1, true><<<grid, 256>>>(P(s), P(s + bytes), nbig, 9u);
+                    });
+                    printf("tail su=%d pct=%2d grid=%6d %8.2f us %7.1f GB/s\n", su, pct, grid, ms * 1e3,
+                           2.0 * tiles * 16384 / (ms * 1e-3) / 1e9);
+                }
+        CK(hipFree(base));
         return 0;
     }
     if (argc > 2 && std::string(argv[2]) == "ways") {
