@@ -164,20 +164,32 @@ std::vector<uint32_t> host_runs(const uint64_t* fs, uint32_t n, uint64_t wire_le
 }
 
 // Run fn(i) for i in [0, parts) on threads of their own (i = 0 on the
-// caller's), each with ctxs[i]'s device current.
+// caller's), each with ctxs[i]'s device current.  fn must not throw (the
+// callers catch inside it); a thread that cannot be started runs its part
+// on the caller's thread afterwards.
 template <class Fn>
 void on_contexts(wsg_ctx* const* ctxs, int parts, Fn fn)
 {
     std::vector<std::thread> th;
-    for (int i = 1; i < parts; ++i)
-        th.emplace_back([&, i] {
-            (void)hipSetDevice(wsg::ctx_device(ctxs[i]));
-            fn(i);
-        });
+    std::vector<int> inline_parts;
+    for (int i = 1; i < parts; ++i) {
+        try {
+            th.emplace_back([&, i] {
+                (void)hipSetDevice(wsg::ctx_device(ctxs[i]));
+                fn(i);
+            });
+        } catch (...) {
+            inline_parts.push_back(i);
+        }
+    }
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(wsg::ctx_device(ctxs[0]));
     fn(0);
+    for (int i : inline_parts) {
+        (void)hipSetDevice(wsg::ctx_device(ctxs[i]));
+        fn(i);
+    }
     (void)hipSetDevice(prev);
     for (auto& t : th)
         t.join();
@@ -368,10 +380,14 @@ uint64_t wsg_mgpu_shard_count(uint64_t n_total, uint32_t chunk, int world, int r
     return shard_count(n_total, chunk, world, rank);
 }
 
-int wsg_mgpu_encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* const* d_payload,
-                           const wsg_send_desc* const* d_desc, const uint32_t* n_local, uint8_t* const* d_wire,
-                           const uint64_t* wire_cap, uint64_t* const* d_wire_off, int root, uint8_t* d_out,
-                           uint64_t out_cap, uint64_t* d_out_off, double* times)
+} // extern "C"
+
+namespace {
+
+int encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* const* d_payload,
+                  const wsg_send_desc* const* d_desc, const uint32_t* n_local, uint8_t* const* d_wire,
+                  const uint64_t* wire_cap, uint64_t* const* d_wire_off, int root, uint8_t* d_out, uint64_t out_cap,
+                  uint64_t* d_out_off, double* times)
 {
     if (!g || chunk == 0 || root < 0 || root >= g->world || !n_local || !d_wire || !wire_cap || !d_wire_off ||
         !d_payload || !d_desc)
@@ -564,8 +580,29 @@ int wsg_mgpu_encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const 
     return WSG_OK;
 }
 
-int wsg_decode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* wire, uint64_t wire_len,
-                                const uint64_t* frame_start, uint32_t n, uint8_t* out, wsg_recv_info* info)
+} // namespace
+
+extern "C" {
+
+int wsg_mgpu_encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* const* d_payload,
+                           const wsg_send_desc* const* d_desc, const uint32_t* n_local, uint8_t* const* d_wire,
+                           const uint64_t* wire_cap, uint64_t* const* d_wire_off, int root, uint8_t* d_out,
+                           uint64_t out_cap, uint64_t* d_out_off, double* times)
+{
+    try {   // no C++ exception leaves the ABI (host vectors: WSG_ENOMEM)
+        return encode_gather(g, n_total, chunk, d_payload, d_desc, n_local, d_wire, wire_cap, d_wire_off, root, d_out,
+                             out_cap, d_out_off, times);
+    } catch (...) {
+        return WSG_ENOMEM;
+    }
+}
+
+} // extern "C"
+
+namespace {
+
+int decode_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* wire, uint64_t wire_len,
+                      const uint64_t* frame_start, uint32_t n, uint8_t* out, wsg_recv_info* info)
 {
     if (!ctxs || nctx <= 0 || (wire_len && (!wire || !out)) || (n && (!frame_start || !info)))
         return WSG_EINVAL;
@@ -589,10 +626,15 @@ int wsg_decode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* w
         if (a == b)
             return;
         const uint64_t lo = a ? frame_start[a] : 0, hi = b < n ? frame_start[b] : wire_len;
-        std::vector<uint64_t> fs(frame_start + a, frame_start + b);
-        for (uint64_t& x : fs)
-            x -= lo;
-        rc[size_t(k)] = wsg_decode_batch_host(ctxs[k], wire + lo, hi - lo, fs.data(), b - a, out + lo, info + a);
+        try {
+            std::vector<uint64_t> fs(frame_start + a, frame_start + b);
+            for (uint64_t& x : fs)
+                x -= lo;
+            rc[size_t(k)] = wsg_decode_batch_host(ctxs[k], wire + lo, hi - lo, fs.data(), b - a, out + lo, info + a);
+        } catch (...) {
+            rc[size_t(k)] = WSG_ENOMEM;
+            return;
+        }
         if (lo)
             for (uint32_t i = a; i < b; ++i)
                 info[i].payload_off += lo;
@@ -618,9 +660,8 @@ int wsg_decode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* w
     return first;
 }
 
-int wsg_encode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* payload, uint64_t payload_len,
-                                const wsg_send_desc* desc, uint32_t n, uint8_t* wire, uint64_t wire_cap,
-                                uint64_t* wire_off)
+int encode_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* payload, uint64_t payload_len,
+                      const wsg_send_desc* desc, uint32_t n, uint8_t* wire, uint64_t wire_cap, uint64_t* wire_off)
 {
     if (!ctxs || nctx <= 0 || !wire_off || (n && (!desc || !wire)) || (payload_len && !payload))
         return WSG_EINVAL;
@@ -656,9 +697,13 @@ int wsg_encode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* p
         const uint32_t a = cut[size_t(k)], b = cut[size_t(k) + 1];
         if (a == b)
             return;
-        std::vector<uint64_t> off(size_t(b - a) + 1);
-        rc[size_t(k)] = wsg_encode_batch_host(ctxs[k], payload, payload_len, desc + a, b - a, wire + wire_off[a],
-                                              wire_off[b] - wire_off[a], off.data());
+        try {
+            std::vector<uint64_t> off(size_t(b - a) + 1);
+            rc[size_t(k)] = wsg_encode_batch_host(ctxs[k], payload, payload_len, desc + a, b - a, wire + wire_off[a],
+                                                  wire_off[b] - wire_off[a], off.data());
+        } catch (...) {
+            rc[size_t(k)] = WSG_ENOMEM;
+        }
     });
     for (int r : rc)
         if (r)
@@ -666,13 +711,43 @@ int wsg_encode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* p
     return WSG_OK;
 }
 
+} // namespace
+
+extern "C" {
+
+// no C++ exception leaves the ABI (allocation failures become WSG_ENOMEM)
+int wsg_decode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* wire, uint64_t wire_len,
+                                const uint64_t* frame_start, uint32_t n, uint8_t* out, wsg_recv_info* info)
+{
+    try {
+        return decode_host_multi(ctxs, nctx, wire, wire_len, frame_start, n, out, info);
+    } catch (...) {
+        return WSG_ENOMEM;
+    }
+}
+
+int wsg_encode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* payload, uint64_t payload_len,
+                                const wsg_send_desc* desc, uint32_t n, uint8_t* wire, uint64_t wire_cap,
+                                uint64_t* wire_off)
+{
+    try {
+        return encode_host_multi(ctxs, nctx, payload, payload_len, desc, n, wire, wire_cap, wire_off);
+    } catch (...) {
+        return WSG_ENOMEM;
+    }
+}
+
 int wsg_mgpu_decode_batch_host(wsg_mgpu* g, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start,
                                uint32_t n, uint8_t* out, wsg_recv_info* info)
 {
     if (!g || g->local.empty())
         return WSG_EINVAL;
-    const std::vector<wsg_ctx*> v = local_ctxs(g);
-    return wsg_decode_batch_host_multi(v.data(), int(v.size()), wire, wire_len, frame_start, n, out, info);
+    try {
+        const std::vector<wsg_ctx*> v = local_ctxs(g);
+        return decode_host_multi(v.data(), int(v.size()), wire, wire_len, frame_start, n, out, info);
+    } catch (...) {
+        return WSG_ENOMEM;
+    }
 }
 
 int wsg_mgpu_encode_batch_host(wsg_mgpu* g, const uint8_t* payload, uint64_t payload_len, const wsg_send_desc* desc,
@@ -680,9 +755,12 @@ int wsg_mgpu_encode_batch_host(wsg_mgpu* g, const uint8_t* payload, uint64_t pay
 {
     if (!g || g->local.empty())
         return WSG_EINVAL;
-    const std::vector<wsg_ctx*> v = local_ctxs(g);
-    return wsg_encode_batch_host_multi(v.data(), int(v.size()), payload, payload_len, desc, n, wire, wire_cap,
-                                       wire_off);
+    try {
+        const std::vector<wsg_ctx*> v = local_ctxs(g);
+        return encode_host_multi(v.data(), int(v.size()), payload, payload_len, desc, n, wire, wire_cap, wire_off);
+    } catch (...) {
+        return WSG_ENOMEM;
+    }
 }
 
 } // extern "C"
