@@ -83,12 +83,14 @@ def lib(path=None):
         "wsg_rx_clear": (ci, [vp, vp]),
         "wsg_rx_forget": (ci, [vp, vp]),
         "wsg_rx_pending": (ci, [vp, ctypes.POINTER(u32), ctypes.POINTER(u64)]),
+        "wsg_rx_set_devices": (ci, [vp, vp, ci]),
         "wsg_rx_flush": (ci, [vp, vp, vp, ctypes.POINTER(u32)]),
         "wsg_tx_create": (ci, [vp, ctypes.POINTER(vp)]),
         "wsg_tx_destroy": (ci, [vp]),
         "wsg_tx_queue": (ci, [vp, vp, ctypes.c_uint8, ci, vp, sz, i32]),
         "wsg_tx_forget": (ci, [vp, vp]),
         "wsg_tx_pending": (ci, [vp, ctypes.POINTER(u32), ctypes.POINTER(u64)]),
+        "wsg_tx_set_devices": (ci, [vp, vp, ci]),
         "wsg_tx_flush": (ci, [vp, vp, vp, ctypes.POINTER(u32)]),
         "wsg_mgpu_create": (ci, [vp, ci, ctypes.POINTER(vp)]),
         "wsg_mgpu_unique_id": (ci, [vp]),
@@ -428,6 +430,11 @@ class RxBatch:
         _check(self._L.wsg_rx_pending(self._rx, ctypes.byref(f), ctypes.byref(b)), "wsg_rx_pending")
         return f.value, b.value
 
+    def set_devices(self, devices):
+        """Spread every flush over these GPUs (wsg_rx_set_devices)."""
+        d = (ctypes.c_int * max(len(devices), 1))(*devices)
+        _check(self._L.wsg_rx_set_devices(self._rx, d, len(devices)), "wsg_rx_set_devices")
+
     def flush(self):
         n = ctypes.c_uint32()
         _check(self._L.wsg_rx_flush(self._rx, self._cb, None, ctypes.byref(n)), "wsg_rx_flush")
@@ -482,6 +489,11 @@ class TxBatch:
         f, b = ctypes.c_uint32(), ctypes.c_uint64()
         _check(self._L.wsg_tx_pending(self._tx, ctypes.byref(f), ctypes.byref(b)), "wsg_tx_pending")
         return f.value, b.value
+
+    def set_devices(self, devices):
+        """Spread every flush over these GPUs (wsg_tx_set_devices)."""
+        d = (ctypes.c_int * max(len(devices), 1))(*devices)
+        _check(self._L.wsg_tx_set_devices(self._tx, d, len(devices)), "wsg_tx_set_devices")
 
     def flush(self):
         n = ctypes.c_uint32()

@@ -441,6 +441,8 @@ void WSServer::EnableBatchReceive(bool on)
         return;
     if (on) {
         _rx_batch = std::make_unique<WSReceiveBatch>(nullptr);   // flushes decode on the flushing thread's codec
+        if (!_batch_devices.empty())
+            _rx_batch->SetDevices(_batch_devices);
         for (auto& s : _sessions)
             s->SetReceiveBatch(_rx_batch.get());
         return;
@@ -448,6 +450,16 @@ void WSServer::EnableBatchReceive(bool on)
     for (auto& s : _sessions)
         s->SetReceiveBatch(nullptr);
     _rx_batch.reset();
+}
+
+void WSServer::SetBatchDevices(const std::vector<int>& devices)
+{
+    std::unique_lock<std::shared_mutex> locker(_sessions_lock);
+    _batch_devices = devices;
+    if (_rx_batch)
+        _rx_batch->SetDevices(devices);
+    if (_tx_batch)
+        _tx_batch->SetDevices(devices);
 }
 
 void WSServer::EnableBatchSend(bool on)
@@ -459,6 +471,8 @@ void WSServer::EnableBatchSend(bool on)
         return;
     if (on) {
         _tx_batch = std::make_unique<WSSendBatch>(nullptr);
+        if (!_batch_devices.empty())
+            _tx_batch->SetDevices(_batch_devices);
         for (auto& s : _sessions)
             s->SetSendBatch(_tx_batch.get());
         return;

@@ -30,6 +30,27 @@ void check(int rc, const char* what)
         throw std::runtime_error(std::string(what) + ": " + wsg_strerror(rc));
 }
 
+// One owned context per device (replacing `ctxs`); contexts of devices
+// already held are kept.
+void set_devices(std::vector<wsg_ctx*>& ctxs, const std::vector<int>& devices)
+{
+    std::vector<wsg_ctx*> next;
+    try {
+        for (int d : devices) {
+            wsg_ctx* c = nullptr;
+            check(wsg_create(d, &c), "wsg_create");
+            next.push_back(c);
+        }
+    } catch (...) {
+        for (wsg_ctx* c : next)
+            wsg_destroy(c);
+        throw;
+    }
+    for (wsg_ctx* c : ctxs)
+        wsg_destroy(c);
+    ctxs.swap(next);
+}
+
 } // namespace
 
 WSReceiveBatch::WSReceiveBatch(wsg_ctx* codec) : _ctx(codec) {}
@@ -40,6 +61,16 @@ WSReceiveBatch::~WSReceiveBatch()
         Release(b->wire);
         Release(b->out);
     }
+    for (wsg_ctx* c : _devs)
+        wsg_destroy(c);
+}
+
+void WSReceiveBatch::SetDevices(const std::vector<int>& devices)
+{
+    std::scoped_lock l(_lock);
+    if (_flushing)
+        throw std::logic_error("WSReceiveBatch::SetDevices during a flush");
+    set_devices(_devs, devices);
 }
 
 void WSReceiveBatch::Grow(Pinned& b, uint64_t need)
@@ -206,9 +237,14 @@ size_t WSReceiveBatch::Flush()
         if (b.keyed) {
             Grow(b.out, b.wire.len);
             payload_base = b.out.p;
-            check(wsg_decode_batch_host(_ctx ? _ctx : ThreadCodec(), b.wire.p, b.wire.len, b.fs.data(),
-                                        uint32_t(n), b.out.p, b.info.data()),
-                  "wsg_decode_batch_host");
+            if (_devs.size() > 1)
+                check(wsg_decode_batch_host_multi(_devs.data(), int(_devs.size()), b.wire.p, b.wire.len, b.fs.data(),
+                                                  uint32_t(n), b.out.p, b.info.data()),
+                      "wsg_decode_batch_host_multi");
+            else
+                check(wsg_decode_batch_host(_devs.size() == 1 ? _devs[0] : _ctx ? _ctx : ThreadCodec(), b.wire.p,
+                                            b.wire.len, b.fs.data(), uint32_t(n), b.out.p, b.info.data()),
+                      "wsg_decode_batch_host");
         } else {
             // no frame has a key to apply (unmasked frames, or key 0: the
             // server-to-client direction of every reference session,
@@ -279,6 +315,16 @@ WSSendBatch::~WSSendBatch()
     for (Pinned* p : {&_q.payload, &_inflight.payload, &_wire})
         if (p->p)
             wsg_host_free(p->p);
+    for (wsg_ctx* c : _devs)
+        wsg_destroy(c);
+}
+
+void WSSendBatch::SetDevices(const std::vector<int>& devices)
+{
+    std::scoped_lock l(_lock);
+    if (_flushing)
+        throw std::logic_error("WSSendBatch::SetDevices during a flush");
+    set_devices(_devs, devices);
 }
 
 void WSSendBatch::Push(Rec rec, uint32_t key, uint8_t opcode, bool mask, const void* buffer, size_t size,
@@ -379,8 +425,12 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
         keyed = keyed || d.key != 0;
     int rc = WSG_OK;
     if (keyed) {
-        rc = wsg_encode_batch_host(_ctx ? _ctx : ThreadCodec(), b.payload.p, b.payload.len, b.desc.data(), n,
-                                   _wire.p, _wire.cap, _wire_off.data());
+        if (_devs.size() > 1)
+            rc = wsg_encode_batch_host_multi(_devs.data(), int(_devs.size()), b.payload.p, b.payload.len,
+                                             b.desc.data(), n, _wire.p, _wire.cap, _wire_off.data());
+        else
+            rc = wsg_encode_batch_host(_devs.size() == 1 ? _devs[0] : _ctx ? _ctx : ThreadCodec(), b.payload.p,
+                                       b.payload.len, b.desc.data(), n, _wire.p, _wire.cap, _wire_off.data());
     } else {
         // every frame has key 0 (server sessions, ws.cpp:206): the XOR is the
         // identity, as on the per-call path; header + status + payload copy
@@ -668,6 +718,20 @@ int wsg_rx_forget(wsg_rx* rx, wsg_session* s)
     return WSG_OK;
 }
 
+int wsg_rx_set_devices(wsg_rx* rx, const int* devices, int n)
+{
+    if (!rx || n < 0 || (n && !devices))
+        return WSG_EINVAL;
+    try {
+        rx->batch.SetDevices(std::vector<int>(devices, devices + n));
+        return WSG_OK;
+    } catch (const std::logic_error&) {
+        return WSG_EINVAL;
+    } catch (...) {
+        return WSG_EHIP;
+    }
+}
+
 int wsg_rx_pending(wsg_rx* rx, uint32_t* frames, uint64_t* bytes)
 {
     if (!rx)
@@ -742,6 +806,20 @@ int wsg_tx_forget(wsg_tx* tx, wsg_session* s)
         return WSG_EINVAL;
     tx->batch.Forget(static_cast<void*>(s));
     return WSG_OK;
+}
+
+int wsg_tx_set_devices(wsg_tx* tx, const int* devices, int n)
+{
+    if (!tx || n < 0 || (n && !devices))
+        return WSG_EINVAL;
+    try {
+        tx->batch.SetDevices(std::vector<int>(devices, devices + n));
+        return WSG_OK;
+    } catch (const std::logic_error&) {
+        return WSG_EINVAL;
+    } catch (...) {
+        return WSG_EHIP;
+    }
 }
 
 int wsg_tx_pending(wsg_tx* tx, uint32_t* frames, uint64_t* payload_bytes)

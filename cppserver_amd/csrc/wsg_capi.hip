@@ -558,32 +558,36 @@ int wsg_fanout_encode_many(wsg_ctx* c, const uint8_t* d_payload, const uint64_t*
                            const uint8_t* opcode, uint32_t m, const uint32_t* d_keys, uint32_t k, int mask,
                            uint8_t* d_wire, uint64_t wire_cap, uint64_t* wire_off, void* stream)
 {
-    if (!c || !wire_off || (m && (!src_off || !len || !opcode)) || (m && k && (!d_keys || !d_wire)))
-        return WSG_EINVAL;
-    if (d_wire && !aligned16(d_wire))
-        return WSG_EINVAL;
-    // message i's frames from wire_off[i], line-aligned (whole-line store rows)
-    uint64_t at = 0;
-    bool any_payload = false;
-    for (uint32_t i = 0; i < m; ++i) {
-        at = (at + wsg::PIECE_ALIGN - 1) & ~(wsg::PIECE_ALIGN - 1);
-        wire_off[i] = at;
-        at += wsg_frame_size(opcode[i], mask, len[i], 0) * k;
-        any_payload = any_payload || len[i] != 0;
-    }
-    wire_off[m] = at;
-    if (at > wire_cap)
-        return WSG_ENOMEM;
-    if (m == 0 || k == 0)
+    try {   // no C++ exception leaves the ABI (host vectors: WSG_ENOMEM)
+        if (!c || !wire_off || (m && (!src_off || !len || !opcode)) || (m && k && (!d_keys || !d_wire)))
+            return WSG_EINVAL;
+        if (d_wire && !aligned16(d_wire))
+            return WSG_EINVAL;
+        // message i's frames from wire_off[i], line-aligned (whole-line store rows)
+        uint64_t at = 0;
+        bool any_payload = false;
+        for (uint32_t i = 0; i < m; ++i) {
+            at = (at + wsg::PIECE_ALIGN - 1) & ~(wsg::PIECE_ALIGN - 1);
+            wire_off[i] = at;
+            at += wsg_frame_size(opcode[i], mask, len[i], 0) * k;
+            any_payload = any_payload || len[i] != 0;
+        }
+        wire_off[m] = at;
+        if (at > wire_cap)
+            return WSG_ENOMEM;
+        if (m == 0 || k == 0)
+            return WSG_OK;
+        if (any_payload && !d_payload)
+            return WSG_EINVAL;
+        hipStream_t s = pick(c, stream);
+        const int t = timing_begin(c, s);
+        if (int rc = fanout_many(c, s, d_payload, src_off, len, opcode, m, d_keys, k, mask, d_wire, wire_off))
+            return rc;
+        timing_end(c, s, t);
         return WSG_OK;
-    if (any_payload && !d_payload)
-        return WSG_EINVAL;
-    hipStream_t s = pick(c, stream);
-    const int t = timing_begin(c, s);
-    if (int rc = fanout_many(c, s, d_payload, src_off, len, opcode, m, d_keys, k, mask, d_wire, wire_off))
-        return rc;
-    timing_end(c, s, t);
-    return WSG_OK;
+    } catch (...) {
+        return WSG_ENOMEM;
+    }
 }
 
 int wsg_xor_host(wsg_ctx* c, const void* src, void* dst, size_t len, uint32_t key, uint32_t phase)
@@ -756,115 +760,119 @@ int wsg_host_free(void* p)
 int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start,
                           uint32_t n, uint8_t* out, wsg_recv_info* info)
 {
-    if (!c || (wire_len && (!wire || !out)) || (n && (!frame_start || !info)))
-        return WSG_EINVAL;
-    if (n == 0) {
-        if (wire_len && out != wire)
-            std::memmove(out, wire, wire_len);
-        return WSG_OK;
-    }
-    uint64_t seg_bytes = 32ull << 20;
-    if (const char* e = std::getenv("WSG_STAGE_MB"))
-        seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
-    const bool in_pinned = host_pinned(wire), out_pinned = host_pinned(out);
+    try {   // no C++ exception leaves the ABI (host vectors: WSG_ENOMEM)
+        if (!c || (wire_len && (!wire || !out)) || (n && (!frame_start || !info)))
+            return WSG_EINVAL;
+        if (n == 0) {
+            if (wire_len && out != wire)
+                std::memmove(out, wire, wire_len);
+            return WSG_OK;
+        }
+        uint64_t seg_bytes = 32ull << 20;
+        if (const char* e = std::getenv("WSG_STAGE_MB"))
+            seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+        const bool in_pinned = host_pinned(wire), out_pinned = host_pinned(out);
 
-    // segments: runs of whole frames of about seg_bytes; segment k covers wire
-    // bytes [start of its first frame, start of the next segment's first frame)
-    std::vector<uint32_t> cut{0};
-    {
-        uint64_t from = 0;
-        for (uint32_t i = 1; i < n; ++i) {
-            if (frame_start[i] >= wire_len)
-                break;   // frames past the wire: error frames, kept with the last segment
-            if (frame_start[i] > from && frame_start[i] - from >= seg_bytes) {
-                cut.push_back(i);
-                from = frame_start[i];
+        // segments: runs of whole frames of about seg_bytes; segment k covers wire
+        // bytes [start of its first frame, start of the next segment's first frame)
+        std::vector<uint32_t> cut{0};
+        {
+            uint64_t from = 0;
+            for (uint32_t i = 1; i < n; ++i) {
+                if (frame_start[i] >= wire_len)
+                    break;   // frames past the wire: error frames, kept with the last segment
+                if (frame_start[i] > from && frame_start[i] - from >= seg_bytes) {
+                    cut.push_back(i);
+                    from = frame_start[i];
+                }
             }
+            cut.push_back(n);
         }
-        cut.push_back(n);
-    }
-    const size_t nseg = cut.size() - 1;
-    uint64_t max_bytes = 0, max_frames = 0;
-    auto seg_lo = [&](size_t k) { return k == 0 ? uint64_t(0) : std::min(frame_start[cut[k]], wire_len); };
-    auto seg_hi = [&](size_t k) { return k + 1 == nseg ? wire_len : std::min(frame_start[cut[k + 1]], wire_len); };
-    for (size_t k = 0; k < nseg; ++k) {
-        const uint64_t base = seg_lo(k) & ~uint64_t(15);
-        max_bytes = std::max(max_bytes, std::max(seg_hi(k), seg_lo(k)) - base);
-        max_frames = std::max<uint64_t>(max_frames, cut[k + 1] - cut[k]);
-    }
-    for (auto& sl : c->slots)
-        if (int rc = slot_reserve(sl, max_bytes, max_frames, !in_pinned || !out_pinned))
-            return rc;
+        const size_t nseg = cut.size() - 1;
+        uint64_t max_bytes = 0, max_frames = 0;
+        auto seg_lo = [&](size_t k) { return k == 0 ? uint64_t(0) : std::min(frame_start[cut[k]], wire_len); };
+        auto seg_hi = [&](size_t k) { return k + 1 == nseg ? wire_len : std::min(frame_start[cut[k + 1]], wire_len); };
+        for (size_t k = 0; k < nseg; ++k) {
+            const uint64_t base = seg_lo(k) & ~uint64_t(15);
+            max_bytes = std::max(max_bytes, std::max(seg_hi(k), seg_lo(k)) - base);
+            max_frames = std::max<uint64_t>(max_frames, cut[k + 1] - cut[k]);
+        }
+        for (auto& sl : c->slots)
+            if (int rc = slot_reserve(sl, max_bytes, max_frames, !in_pinned || !out_pinned))
+                return rc;
 
-    for (size_t k = 0; k < nseg; ++k) {
-        wsg_ctx::Slot& sl = c->slots[k % wsg_ctx::kSlots];
-        if (int rc = slot_drain(sl))
-            return rc;
-        const uint32_t i0 = cut[k], i1 = cut[k + 1], m = i1 - i0;
-        const uint64_t lo = seg_lo(k), hi = std::max(seg_hi(k), lo);
-        const uint64_t base = lo & ~uint64_t(15);   // 16-B aligned device copy of [base, hi)
-        const uint64_t len = hi - base;
-        for (uint32_t j = 0; j < m; ++j)
-            sl.h_fs[j] = frame_start[i0 + j] >= base ? frame_start[i0 + j] - base : ~uint64_t(0);
-        const uint8_t* src = wire + base;
-        if (!in_pinned) {
-            std::memcpy(sl.h_in, wire + base, len);
-            src = sl.h_in;
+        for (size_t k = 0; k < nseg; ++k) {
+            wsg_ctx::Slot& sl = c->slots[k % wsg_ctx::kSlots];
+            if (int rc = slot_drain(sl))
+                return rc;
+            const uint32_t i0 = cut[k], i1 = cut[k + 1], m = i1 - i0;
+            const uint64_t lo = seg_lo(k), hi = std::max(seg_hi(k), lo);
+            const uint64_t base = lo & ~uint64_t(15);   // 16-B aligned device copy of [base, hi)
+            const uint64_t len = hi - base;
+            for (uint32_t j = 0; j < m; ++j)
+                sl.h_fs[j] = frame_start[i0 + j] >= base ? frame_start[i0 + j] - base : ~uint64_t(0);
+            const uint8_t* src = wire + base;
+            if (!in_pinned) {
+                std::memcpy(sl.h_in, wire + base, len);
+                src = sl.h_in;
+            }
+            Pipe pp;
+            if (int rc = pipe_for(c, sl, pp))
+                return rc;
+            WSG_HIP(hipMemcpyAsync(sl.d_wire, src, len, hipMemcpyHostToDevice, pp.h2d));
+            WSG_HIP(hipMemcpyAsync(sl.d_fs, sl.h_fs, m * sizeof(uint64_t), hipMemcpyHostToDevice, pp.h2d));
+            if (int rc = pipe_to_kern(pp, sl))
+                return rc;
+            if (int rc = decode_launch(c, sl.d_wire, len, sl.d_fs, m, sl.d_wire, sl.d_info, pp.kern, c->d_err_host))
+                return rc;
+            if (int rc = pipe_to_d2h(pp, sl))
+                return rc;
+            // copy back [lo, hi): bytes before lo belong to the previous segment
+            const uint64_t back = hi - lo;
+            if (out_pinned) {
+                WSG_HIP(hipMemcpyAsync(out + lo, sl.d_wire + (lo - base), back, hipMemcpyDeviceToHost, pp.d2h));
+                sl.out_dst = nullptr;
+            } else {
+                WSG_HIP(hipMemcpyAsync(sl.h_out, sl.d_wire + (lo - base), back, hipMemcpyDeviceToHost, pp.d2h));
+                sl.out_dst = out + lo;
+                sl.out_src = 0;
+            }
+            sl.out_len = back;
+            WSG_HIP(hipMemcpyAsync(sl.h_info, sl.d_info, m * sizeof(wsg_recv_info), hipMemcpyDeviceToHost, pp.d2h));
+            sl.info_dst = info + i0;
+            sl.info_n = m;
+            sl.base = base;
+            WSG_HIP(hipEventRecord(sl.done, pp.d2h));
+            sl.busy = true;
         }
-        Pipe pp;
-        if (int rc = pipe_for(c, sl, pp))
-            return rc;
-        WSG_HIP(hipMemcpyAsync(sl.d_wire, src, len, hipMemcpyHostToDevice, pp.h2d));
-        WSG_HIP(hipMemcpyAsync(sl.d_fs, sl.h_fs, m * sizeof(uint64_t), hipMemcpyHostToDevice, pp.h2d));
-        if (int rc = pipe_to_kern(pp, sl))
-            return rc;
-        if (int rc = decode_launch(c, sl.d_wire, len, sl.d_fs, m, sl.d_wire, sl.d_info, pp.kern, c->d_err_host))
-            return rc;
-        if (int rc = pipe_to_d2h(pp, sl))
-            return rc;
-        // copy back [lo, hi): bytes before lo belong to the previous segment
-        const uint64_t back = hi - lo;
-        if (out_pinned) {
-            WSG_HIP(hipMemcpyAsync(out + lo, sl.d_wire + (lo - base), back, hipMemcpyDeviceToHost, pp.d2h));
-            sl.out_dst = nullptr;
-        } else {
-            WSG_HIP(hipMemcpyAsync(sl.h_out, sl.d_wire + (lo - base), back, hipMemcpyDeviceToHost, pp.d2h));
-            sl.out_dst = out + lo;
-            sl.out_src = 0;
-        }
-        sl.out_len = back;
-        WSG_HIP(hipMemcpyAsync(sl.h_info, sl.d_info, m * sizeof(wsg_recv_info), hipMemcpyDeviceToHost, pp.d2h));
-        sl.info_dst = info + i0;
-        sl.info_n = m;
-        sl.base = base;
-        WSG_HIP(hipEventRecord(sl.done, pp.d2h));
-        sl.busy = true;
-    }
-    for (auto& sl : c->slots)
-        if (int rc = slot_drain(sl))
-            return rc;
-    // the pipeline's kernels latched into d_err_host (segment-relative frame
-    // indices, meaningless to the caller); the status comes from the
-    // per-frame errors below, and the caller's own latch is left alone
+        for (auto& sl : c->slots)
+            if (int rc = slot_drain(sl))
+                return rc;
+        // the pipeline's kernels latched into d_err_host (segment-relative frame
+        // indices, meaningless to the caller); the status comes from the
+        // per-frame errors below, and the caller's own latch is left alone
 
-    // batch semantics: a frame that runs into the next segment's first frame
-    // overlaps it (EINVAL), it is not truncated; and the status is the error
-    // of the lowest-indexed bad frame
-    int first = WSG_OK;
-    for (uint32_t i = 0; i < n; ++i) {
-        wsg_recv_info& r = info[i];
-        if (r.error == WSG_ETRUNC && i + 1 < n && frame_start[i] < wire_len) {
-            wsg_recv_info h;
-            if (wsg_header_unpack(wire + frame_start[i], wire_len - frame_start[i], &h) == WSG_OK &&
-                h.len <= wire_len - frame_start[i] - h.hdr_len)
-                r.error = int8_t(WSG_EINVAL);
+        // batch semantics: a frame that runs into the next segment's first frame
+        // overlaps it (EINVAL), it is not truncated; and the status is the error
+        // of the lowest-indexed bad frame
+        int first = WSG_OK;
+        for (uint32_t i = 0; i < n; ++i) {
+            wsg_recv_info& r = info[i];
+            if (r.error == WSG_ETRUNC && i + 1 < n && frame_start[i] < wire_len) {
+                wsg_recv_info h;
+                if (wsg_header_unpack(wire + frame_start[i], wire_len - frame_start[i], &h) == WSG_OK &&
+                    h.len <= wire_len - frame_start[i] - h.hdr_len)
+                    r.error = int8_t(WSG_EINVAL);
+            }
+            if (r.error && !first)
+                first = r.error;
         }
-        if (r.error && !first)
-            first = r.error;
+        if (first)   // re-arm the pipeline's latch (every slot has drained)
+            WSG_HIP(hipMemset(c->d_err_host, 0xFF, sizeof(unsigned long long)));
+        return first;
+    } catch (...) {
+        return WSG_ENOMEM;
     }
-    if (first)   // re-arm the pipeline's latch (every slot has drained)
-        WSG_HIP(hipMemset(c->d_err_host, 0xFF, sizeof(unsigned long long)));
-    return first;
 }
 
 namespace {
@@ -914,129 +922,133 @@ int slot_reserve_enc(wsg_ctx::Slot& sl, uint64_t payload_bytes, uint64_t wire_by
 int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_len, const wsg_send_desc* desc,
                           uint32_t n, uint8_t* wire, uint64_t wire_cap, uint64_t* wire_off)
 {
-    if (!c || !wire_off || (n && (!desc || !wire)) || (payload_len && !payload))
-        return WSG_EINVAL;
-    // frame offsets on the host (the same arithmetic as k_encode_scan_*), so
-    // that segments can be cut and copied back without a device round trip
-    wire_off[0] = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        const wsg_send_desc& d = desc[i];
-        if (d.len > payload_len || d.src_off > payload_len - d.len)
+    try {   // no C++ exception leaves the ABI (host vectors: WSG_ENOMEM)
+        if (!c || !wire_off || (n && (!desc || !wire)) || (payload_len && !payload))
             return WSG_EINVAL;
-        wire_off[i + 1] = wire_off[i] + wsg_frame_size(d.opcode, d.mask, d.len, d.status);
-    }
-    if (wire_off[n] > wire_cap)
-        return WSG_ENOMEM;
-    if (n == 0)
-        return WSG_OK;
-    uint64_t seg_bytes = 32ull << 20;
-    if (const char* e = std::getenv("WSG_STAGE_MB"))
-        seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
-    const bool in_pinned = host_pinned(payload), out_pinned = host_pinned(wire);
+        // frame offsets on the host (the same arithmetic as k_encode_scan_*), so
+        // that segments can be cut and copied back without a device round trip
+        wire_off[0] = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            const wsg_send_desc& d = desc[i];
+            if (d.len > payload_len || d.src_off > payload_len - d.len)
+                return WSG_EINVAL;
+            wire_off[i + 1] = wire_off[i] + wsg_frame_size(d.opcode, d.mask, d.len, d.status);
+        }
+        if (wire_off[n] > wire_cap)
+            return WSG_ENOMEM;
+        if (n == 0)
+            return WSG_OK;
+        uint64_t seg_bytes = 32ull << 20;
+        if (const char* e = std::getenv("WSG_STAGE_MB"))
+            seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+        const bool in_pinned = host_pinned(payload), out_pinned = host_pinned(wire);
 
-    // segments of whole frames, ~seg_bytes of wire each
-    struct Seg {
-        uint32_t i0, i1;
-        uint64_t lo, hi;   // payload source range [lo, hi) (16-B aligned lo)
-        uint64_t sum;      // payload bytes of its frames
-        bool gather;       // frames' payloads not one tight range: copy them together
-    };
-    std::vector<Seg> segs;
-    for (uint32_t i0 = 0; i0 < n;) {
-        Seg g{i0, i0, ~uint64_t(0), 0, 0, false};
-        do {
-            const wsg_send_desc& d = desc[g.i1];
-            if (d.len) {
-                g.lo = std::min(g.lo, d.src_off);
-                g.hi = std::max(g.hi, d.src_off + d.len);
-            }
-            g.sum += d.len;
-            ++g.i1;
-        } while (g.i1 < n && wire_off[g.i1] - wire_off[i0] < seg_bytes);
-        if (g.lo > g.hi)
-            g.lo = g.hi = 0;
-        g.lo &= ~uint64_t(15);
-        g.gather = g.hi - g.lo > g.sum + 16 * uint64_t(g.i1 - g.i0) + 4096;
-        segs.push_back(g);
-        i0 = g.i1;
-    }
-    uint64_t max_payload = 0, max_wire = 0;
-    uint32_t max_frames = 0;
-    bool need_host = !out_pinned;
-    for (const Seg& g : segs) {
-        max_payload = std::max(max_payload, g.gather ? g.sum : g.hi - g.lo);
-        max_wire = std::max(max_wire, wire_off[g.i1] - wire_off[g.i0]);
-        max_frames = std::max(max_frames, g.i1 - g.i0);
-        need_host = need_host || g.gather || !in_pinned;
-    }
-    for (auto& sl : c->slots)
-        if (int rc = slot_reserve_enc(sl, max_payload, max_wire, max_frames, need_host))
-            return rc;
+        // segments of whole frames, ~seg_bytes of wire each
+        struct Seg {
+            uint32_t i0, i1;
+            uint64_t lo, hi;   // payload source range [lo, hi) (16-B aligned lo)
+            uint64_t sum;      // payload bytes of its frames
+            bool gather;       // frames' payloads not one tight range: copy them together
+        };
+        std::vector<Seg> segs;
+        for (uint32_t i0 = 0; i0 < n;) {
+            Seg g{i0, i0, ~uint64_t(0), 0, 0, false};
+            do {
+                const wsg_send_desc& d = desc[g.i1];
+                if (d.len) {
+                    g.lo = std::min(g.lo, d.src_off);
+                    g.hi = std::max(g.hi, d.src_off + d.len);
+                }
+                g.sum += d.len;
+                ++g.i1;
+            } while (g.i1 < n && wire_off[g.i1] - wire_off[i0] < seg_bytes);
+            if (g.lo > g.hi)
+                g.lo = g.hi = 0;
+            g.lo &= ~uint64_t(15);
+            g.gather = g.hi - g.lo > g.sum + 16 * uint64_t(g.i1 - g.i0) + 4096;
+            segs.push_back(g);
+            i0 = g.i1;
+        }
+        uint64_t max_payload = 0, max_wire = 0;
+        uint32_t max_frames = 0;
+        bool need_host = !out_pinned;
+        for (const Seg& g : segs) {
+            max_payload = std::max(max_payload, g.gather ? g.sum : g.hi - g.lo);
+            max_wire = std::max(max_wire, wire_off[g.i1] - wire_off[g.i0]);
+            max_frames = std::max(max_frames, g.i1 - g.i0);
+            need_host = need_host || g.gather || !in_pinned;
+        }
+        for (auto& sl : c->slots)
+            if (int rc = slot_reserve_enc(sl, max_payload, max_wire, max_frames, need_host))
+                return rc;
 
-    for (size_t k = 0; k < segs.size(); ++k) {
-        const Seg& g = segs[k];
-        wsg_ctx::Slot& sl = c->slots[k % wsg_ctx::kSlots];
-        if (int rc = slot_drain(sl))
-            return rc;
-        const uint32_t m = g.i1 - g.i0;
-        const uint8_t* src = payload + g.lo;
-        uint64_t plen = g.hi - g.lo;
-        if (g.gather) {
-            uint64_t at = 0;
-            for (uint32_t j = 0; j < m; ++j) {
-                wsg_send_desc d = desc[g.i0 + j];
-                if (d.len)
-                    std::memcpy(sl.h_in + at, payload + d.src_off, d.len);
-                d.src_off = at;
-                sl.h_desc[j] = d;
-                at += d.len;
-            }
-            src = sl.h_in;
-            plen = at;
-        } else {
-            for (uint32_t j = 0; j < m; ++j) {
-                wsg_send_desc d = desc[g.i0 + j];
-                d.src_off = d.len ? d.src_off - g.lo : 0;
-                sl.h_desc[j] = d;
-            }
-            if (!in_pinned && plen) {
-                std::memcpy(sl.h_in, src, plen);
+        for (size_t k = 0; k < segs.size(); ++k) {
+            const Seg& g = segs[k];
+            wsg_ctx::Slot& sl = c->slots[k % wsg_ctx::kSlots];
+            if (int rc = slot_drain(sl))
+                return rc;
+            const uint32_t m = g.i1 - g.i0;
+            const uint8_t* src = payload + g.lo;
+            uint64_t plen = g.hi - g.lo;
+            if (g.gather) {
+                uint64_t at = 0;
+                for (uint32_t j = 0; j < m; ++j) {
+                    wsg_send_desc d = desc[g.i0 + j];
+                    if (d.len)
+                        std::memcpy(sl.h_in + at, payload + d.src_off, d.len);
+                    d.src_off = at;
+                    sl.h_desc[j] = d;
+                    at += d.len;
+                }
                 src = sl.h_in;
+                plen = at;
+            } else {
+                for (uint32_t j = 0; j < m; ++j) {
+                    wsg_send_desc d = desc[g.i0 + j];
+                    d.src_off = d.len ? d.src_off - g.lo : 0;
+                    sl.h_desc[j] = d;
+                }
+                if (!in_pinned && plen) {
+                    std::memcpy(sl.h_in, src, plen);
+                    src = sl.h_in;
+                }
             }
+            Pipe pp;
+            if (int rc = pipe_for(c, sl, pp))
+                return rc;
+            if (plen)
+                WSG_HIP(hipMemcpyAsync(sl.d_payload, src, plen, hipMemcpyHostToDevice, pp.h2d));
+            WSG_HIP(hipMemcpyAsync(sl.d_desc, sl.h_desc, m * sizeof(wsg_send_desc), hipMemcpyHostToDevice, pp.h2d));
+            if (int rc = pipe_to_kern(pp, sl))
+                return rc;
+            const uint64_t wlen = wire_off[g.i1] - wire_off[g.i0];
+            if (int rc = encode_launch(c, pp.kern, sl.d_payload, sl.d_desc, m, sl.d_wire, wlen, sl.d_woff, sl.enc,
+                                       c->d_err_host))
+                return rc;
+            if (int rc = pipe_to_d2h(pp, sl))
+                return rc;
+            if (out_pinned) {
+                WSG_HIP(hipMemcpyAsync(wire + wire_off[g.i0], sl.d_wire, wlen, hipMemcpyDeviceToHost, pp.d2h));
+                sl.out_dst = nullptr;
+            } else {
+                WSG_HIP(hipMemcpyAsync(sl.h_out, sl.d_wire, wlen, hipMemcpyDeviceToHost, pp.d2h));
+                sl.out_dst = wire + wire_off[g.i0];
+                sl.out_src = 0;
+            }
+            sl.out_len = wlen;
+            sl.info_n = 0;
+            WSG_HIP(hipEventRecord(sl.done, pp.d2h));
+            sl.busy = true;
         }
-        Pipe pp;
-        if (int rc = pipe_for(c, sl, pp))
-            return rc;
-        if (plen)
-            WSG_HIP(hipMemcpyAsync(sl.d_payload, src, plen, hipMemcpyHostToDevice, pp.h2d));
-        WSG_HIP(hipMemcpyAsync(sl.d_desc, sl.h_desc, m * sizeof(wsg_send_desc), hipMemcpyHostToDevice, pp.h2d));
-        if (int rc = pipe_to_kern(pp, sl))
-            return rc;
-        const uint64_t wlen = wire_off[g.i1] - wire_off[g.i0];
-        if (int rc = encode_launch(c, pp.kern, sl.d_payload, sl.d_desc, m, sl.d_wire, wlen, sl.d_woff, sl.enc,
-                                   c->d_err_host))
-            return rc;
-        if (int rc = pipe_to_d2h(pp, sl))
-            return rc;
-        if (out_pinned) {
-            WSG_HIP(hipMemcpyAsync(wire + wire_off[g.i0], sl.d_wire, wlen, hipMemcpyDeviceToHost, pp.d2h));
-            sl.out_dst = nullptr;
-        } else {
-            WSG_HIP(hipMemcpyAsync(sl.h_out, sl.d_wire, wlen, hipMemcpyDeviceToHost, pp.d2h));
-            sl.out_dst = wire + wire_off[g.i0];
-            sl.out_src = 0;
-        }
-        sl.out_len = wlen;
-        sl.info_n = 0;
-        WSG_HIP(hipEventRecord(sl.done, pp.d2h));
-        sl.busy = true;
+        for (auto& sl : c->slots)
+            if (int rc = slot_drain(sl))
+                return rc;
+        // the encode kernels latch only capacity errors, and capacity was checked
+        // on the host above: nothing for the pipeline's latch to report
+        return WSG_OK;
+    } catch (...) {
+        return WSG_ENOMEM;
     }
-    for (auto& sl : c->slots)
-        if (int rc = slot_drain(sl))
-            return rc;
-    // the encode kernels latch only capacity errors, and capacity was checked
-    // on the host above: nothing for the pipeline's latch to report
-    return WSG_OK;
 }
 
 uint64_t wsg_frame_size(uint8_t opcode, int mask, uint64_t len, int32_t status)

@@ -57,6 +57,10 @@ public:
     //! order; returns the number of frames delivered.  A Flush() called from
     //! inside a callback returns 0 (its frames go with the next one).
     size_t Flush();
+    //! Spread every flush's GPU pass over these devices' PCIe links
+    //! (wsg_decode_batch_host_multi: one context per device, owned by the
+    //! batch); empty: the batch's own context.  Not during a flush.
+    void SetDevices(const std::vector<int>& devices);
 
     size_t frames() const
     {
@@ -100,6 +104,7 @@ private:
     static void Release(Pinned& b);
 
     wsg_ctx* _ctx;
+    std::vector<wsg_ctx*> _devs;   // SetDevices: owned, one per device
     Batch _cur, _spare;
     bool _flushing = false;
     mutable std::mutex _lock;   // _cur, the records of _spare, _flushing
@@ -147,6 +152,10 @@ public:
     //! Encode everything queued and hand the frames out in queue order;
     //! returns the number of frames handed out
     size_t Flush(Sink sink = nullptr, void* user = nullptr);
+    //! Spread every flush's GPU pass over these devices' PCIe links
+    //! (wsg_encode_batch_host_multi; contexts owned by the batch); empty:
+    //! the batch's own context.  Not during a flush.
+    void SetDevices(const std::vector<int>& devices);
 
     size_t frames() const
     {
@@ -178,6 +187,7 @@ private:
     };
 
     wsg_ctx* _ctx;
+    std::vector<wsg_ctx*> _devs;   // SetDevices: owned, one per device
     Queue_ _q, _inflight;   // frames being queued | the frames a flush is encoding
     Pinned _wire;
     std::vector<uint64_t> _wire_off;

@@ -64,11 +64,17 @@ public:
     bool IsBatchSend() const { return _tx_batch != nullptr; }
     size_t FlushSend();
 
+    //! The GPUs the batched flushes spread over (one run per device's PCIe
+    //! link, wsg_*_batch_host_multi); empty (default): the flushing
+    //! thread's GPU.  Applies to the batches enabled now and later.
+    void SetBatchDevices(const std::vector<int>& devices);
+
 private:
     size_t MulticastFrame(uint8_t opcode, const void* buffer, size_t size);
 
     std::unique_ptr<WSReceiveBatch> _rx_batch;
     std::unique_ptr<WSSendBatch> _tx_batch;
+    std::vector<int> _batch_devices;
 
     mutable std::shared_mutex _sessions_lock;
     std::vector<std::shared_ptr<WSSession>> _sessions;

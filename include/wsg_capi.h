@@ -229,6 +229,10 @@ int wsg_rx_feed(wsg_rx* rx, wsg_session* s, const void* buf, size_t size);
 int wsg_rx_clear(wsg_rx* rx, wsg_session* s);
 /* Drop a session's queued frames (before wsg_session_destroy).                */
 int wsg_rx_forget(wsg_rx* rx, wsg_session* s);
+/* Spread every flush's GPU pass over these devices' PCIe links (one context
+ * per device, owned by rx; wsg_decode_batch_host_multi); n = 0: rx's own ctx.
+ * Not from inside a flush (WSG_EINVAL).                                       */
+int wsg_rx_set_devices(wsg_rx* rx, const int* devices, int n);
 /* Complete frames and wire bytes queued for the next flush.                   */
 int wsg_rx_pending(wsg_rx* rx, uint32_t* frames, uint64_t* bytes);
 int wsg_rx_flush(wsg_rx* rx, wsg_rx_cb cb, void* user, uint32_t* delivered);
@@ -248,6 +252,8 @@ int wsg_tx_queue(wsg_tx* tx, wsg_session* s, uint8_t opcode, int mask,
                  const void* buf, size_t size, int32_t status);
 /* Drop a session's queued frames (before wsg_session_destroy).                */
 int wsg_tx_forget(wsg_tx* tx, wsg_session* s);
+/* The same for the send batch (wsg_encode_batch_host_multi).                 */
+int wsg_tx_set_devices(wsg_tx* tx, const int* devices, int n);
 int wsg_tx_pending(wsg_tx* tx, uint32_t* frames, uint64_t* payload_bytes);
 int wsg_tx_flush(wsg_tx* tx, wsg_tx_sink sink, void* user, uint32_t* sent);
 

@@ -305,7 +305,7 @@ static void test_soak()
 // Server-side batched receive: sessions' bytes are
 // framed into one batch and unmasked in one GPU pass per FlushReceived();
 // callbacks (and so the echoes) happen only at the flush, in arrival order.
-static void test_batched_server_receive()
+static void test_batched_server_receive(const std::vector<int>& devices = {})
 {
     WSServer server;
     std::vector<std::unique_ptr<Pair>> pairs;
@@ -314,6 +314,8 @@ static void test_batched_server_receive()
         server.AddSession(pairs.back()->session);
     }
     server.EnableBatchReceive(true);
+    if (!devices.empty())
+        server.SetBatchDevices(devices);   // flushes spread over these GPUs' links
     CHECK(server.IsBatchReceive());
     std::mt19937 gen(99);
     std::vector<std::vector<std::vector<uint8_t>>> sent(pairs.size());
@@ -746,6 +748,11 @@ int main()
         test_connect_async();
         test_soak();
         test_batched_server_receive();
+        // the same with every flush split over three contexts of the one GPU
+        // (as over three GPUs: wsg_decode_batch_host_multi)
+        setenv("WSG_HOST_MULTI_SHARE", "1", 1);
+        test_batched_server_receive({0, 0, 0});
+        unsetenv("WSG_HOST_MULTI_SHARE");
         test_batched_send();
         test_auto_batch_echo();
         test_multicast_tick();

@@ -37,7 +37,7 @@ def _stream(rng, n, max_len, masked_p=0.7):
     return b"".join(out)
 
 
-def _run(codec, rng, streams, chunk, flush_p):
+def _run(codec, rng, streams, chunk, flush_p, devices=None):
     """Feed `streams` interleaved in random chunks to the oracle (per call) and
     to one RxBatch; return (expected events, batch events)."""
     S = len(streams)
@@ -45,6 +45,8 @@ def _run(codec, rng, streams, chunk, flush_p):
     prod = [ca.Session(codec) for _ in range(S)]
     index = {id(p): i for i, p in enumerate(prod)}
     rx = ca.RxBatch(codec)
+    if devices is not None:
+        rx.set_devices(devices)
     pos = [0] * S
     expect = []
     while True:
@@ -74,6 +76,19 @@ def test_rx_batch_interleaved_vs_oracle(codec, seed, chunk, flush_p):
     rng = np.random.default_rng(seed)
     streams = [_stream(rng, 40, 3000) for _ in range(16)]
     expect, got = _run(codec, rng, streams, chunk, flush_p)
+    assert len(expect) > 0
+    assert got == expect
+
+
+@pytest.mark.parametrize("seed,chunk", [(31, None), (32, 700)])
+def test_rx_batch_over_devices_vs_oracle(codec, seed, chunk, monkeypatch):
+    """Flushes spread over several contexts (wsg_rx_set_devices; two of the
+    one GPU, split as distinct GPUs would be): the same callbacks in the same
+    order."""
+    monkeypatch.setenv("WSG_HOST_MULTI_SHARE", "1")
+    rng = np.random.default_rng(seed)
+    streams = [_stream(rng, 40, 20000) for _ in range(16)]
+    expect, got = _run(codec, rng, streams, chunk, 0.05, devices=[0, 0, 0])
     assert len(expect) > 0
     assert got == expect
 

@@ -95,14 +95,19 @@ def test_encode_batch_host_errors(codec):
     assert rc == ca.WSG_ENOMEM
 
 
-def test_tx_batch_vs_oracle(codec):
+@pytest.mark.parametrize("devices", [None, [0, 0, 0]])
+def test_tx_batch_vs_oracle(codec, devices, monkeypatch):
     """Many sessions with their own keys queue random frames; one flush hands
-    back every frame in queue order, each equal to the per-call encode."""
+    back every frame in queue order, each equal to the per-call encode (also
+    with the flush spread over several contexts, wsg_tx_set_devices)."""
+    monkeypatch.setenv("WSG_HOST_MULTI_SHARE", "1")
     rng = np.random.default_rng(33)
     S = 20
     sessions = [ca.Session(codec, int(rng.integers(0, 2**32))) for _ in range(S)]
     refs = [oracle.Session() for _ in range(S)]
     tx = ca.TxBatch(codec)
+    if devices is not None:
+        tx.set_devices(devices)
     expect = []
     for _ in range(400):
         i = int(rng.integers(0, S))
