@@ -13,7 +13,10 @@ constexpr int CHUNK = 16;                   // bytes per lane per step (dwordx4)
 #endif
 constexpr int UNROLL = WSG_UNROLL;          // steps per lane per tile
 constexpr uint64_t TILE = uint64_t(BLOCK) * CHUNK * UNROLL;   // 16 KiB of output
-constexpr int EU = 4;                                   // encode: 16-B steps per lane per piece
+#ifndef WSG_EU
+#define WSG_EU 4
+#endif
+constexpr int EU = WSG_EU;                              // encode: 16-B steps per lane per piece
 constexpr uint64_t PIECE = uint64_t(64) * CHUNK * EU;   // encode work piece: 4 KiB of one frame
 // Pieces start on 128-byte line boundaries of the OUTPUT, so every 1 KiB
 // store row of a wave writes whole lines (a 16-B-aligned but line-misaligned
