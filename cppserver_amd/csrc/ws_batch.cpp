@@ -11,6 +11,7 @@
 #include "ws_session_impl.h"
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -528,33 +529,49 @@ AutoState& auto_state()
 }
 
 // AtEnd registrations: (thread, key, fn), process-wide so that Cancel works
-// from any thread
+// from any thread.  A hook being run is listed in g_end_running until it
+// returns, and Cancel from another thread waits for it: the object can be
+// destroyed only after its hook is done with it.
 struct EndHook {
     std::thread::id thread;
     void* key;
     void (*fn)(void*);
 };
 std::mutex g_end_lock;
+std::condition_variable g_end_done;
 std::vector<EndHook> g_end_hooks;
+std::vector<EndHook> g_end_running;
 
 void run_end_hooks()
 {
-    std::vector<EndHook> mine;
-    {
-        std::lock_guard<std::mutex> g(g_end_lock);
-        const auto me = std::this_thread::get_id();
-        for (size_t i = 0; i < g_end_hooks.size();) {
-            if (g_end_hooks[i].thread == me) {
-                mine.push_back(g_end_hooks[i]);
-                g_end_hooks[i] = g_end_hooks.back();
-                g_end_hooks.pop_back();
-            } else {
-                ++i;
-            }
+    const auto me = std::this_thread::get_id();
+    for (;;) {
+        EndHook h;
+        {
+            std::lock_guard<std::mutex> g(g_end_lock);
+            auto it = std::find_if(g_end_hooks.begin(), g_end_hooks.end(),
+                                   [&](const EndHook& e) { return e.thread == me; });
+            if (it == g_end_hooks.end())
+                return;
+            h = *it;
+            g_end_hooks.erase(it);
+            g_end_running.push_back(h);
         }
-    }
-    for (const EndHook& h : mine)
+        struct Finish {
+            const EndHook& h;
+            ~Finish()
+            {
+                std::lock_guard<std::mutex> g(g_end_lock);
+                for (size_t i = 0; i < g_end_running.size(); ++i)
+                    if (g_end_running[i].key == h.key && g_end_running[i].thread == h.thread) {
+                        g_end_running.erase(g_end_running.begin() + std::ptrdiff_t(i));
+                        break;
+                    }
+                g_end_done.notify_all();
+            }
+        } finish{h};
         h.fn(h.key);
+    }
 }
 
 } // namespace
@@ -587,7 +604,7 @@ void BatchScope::AtEnd(void* key, void (*fn)(void*))
 
 void BatchScope::Cancel(void* key)
 {
-    std::lock_guard<std::mutex> g(g_end_lock);
+    std::unique_lock<std::mutex> g(g_end_lock);
     for (size_t i = 0; i < g_end_hooks.size();) {
         if (g_end_hooks[i].key == key) {
             g_end_hooks[i] = g_end_hooks.back();
@@ -596,6 +613,13 @@ void BatchScope::Cancel(void* key)
             ++i;
         }
     }
+    // a hook of `key` running on another thread finishes first (on this
+    // thread it is the caller itself: nothing to wait for)
+    const auto me = std::this_thread::get_id();
+    g_end_done.wait(g, [&] {
+        return std::none_of(g_end_running.begin(), g_end_running.end(),
+                            [&](const EndHook& e) { return e.key == key && e.thread != me; });
+    });
 }
 
 size_t BatchScope::Flush()
