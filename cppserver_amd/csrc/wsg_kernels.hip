@@ -65,6 +65,9 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_DEC_INFO_LAST
 #define WSG_DEC_INFO_LAST 0   // k_decode: per-frame info slice after the tiles, on the grid's last blocks (A/B)
 #endif
+#ifndef WSG_DEC_PAIR
+#define WSG_DEC_PAIR 0   // k_decode: two tiles per block, both loaded up front (A/B with WSG_DEC_TILES_PER_BLOCK=2)
+#endif
 #ifndef WSG_FAN_PERIOD
 #define WSG_FAN_PERIOD 1   // fan-out: period path (k_fanout_period) where the frame size allows; 0 = flat kernel only
 #endif
@@ -479,6 +482,240 @@ __device__ __forceinline__ v4u seg_xor(uint32_t o, const Seg& s)
     return m;
 }
 
+// A tile's inputs, issued before its metadata chain: the coarse probe of
+// the frame table (vector load, first: loads return in issue order) and the
+// tile's data.
+struct TileIn {
+    uint64_t base, g, probe;
+    v4u v[UNROLL];
+};
+
+__device__ __forceinline__ void load_tile(TileIn& T, const uint8_t* __restrict__ wire, uint64_t wire_len,
+                                          const uint64_t* __restrict__ fs, uint32_t n, double frames_per_byte,
+                                          uint32_t stride, uint64_t base)
+{
+    T.base = base;
+    T.g = tile_guess(n, frames_per_byte, base);
+#if WSG_DIAG == 7   // timing-only: no coarse probe (right only where the guess is exact: equal-size frames)
+    T.probe = 0;
+#else
+    T.probe = fs[probe_index(T.g, stride, n, int(threadIdx.x & 63))];
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+    // the tile's data does not depend on frame metadata: issue it next,
+    // unconditionally, so that the metadata chain waits for the probe alone
+    // (vmcnt(UNROLL)); loads behind a branch made the compiler wait vmcnt(0)
+    // there, i.e. start the chain only once the whole tile had arrived.  The
+    // wire's last, partial tile takes the staged path, which reads its bytes
+    // itself: its loads here are clamped to the 16-B block holding the last
+    // wire byte (readable by contract) and their values are not used.
+    const uint64_t last_blk = (wire_len - 1) & ~uint64_t(CHUNK - 1);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+        T.v[u] = ld16nt(wire + min(base + lane_off(u), last_blk));
+}
+
+// The tile's frames located, their segments XORed into its bytes, stored.
+__device__ __forceinline__ void process_tile(const TileIn& T, const uint8_t* __restrict__ wire, uint8_t* out,
+                                             uint64_t wire_len, const uint64_t* __restrict__ fs, uint32_t n,
+                                             uint32_t stride)
+{
+    const uint64_t base = T.base;
+    const uint64_t tend = min(base + TILE, wire_len);
+    const uint32_t span = uint32_t(tend - base);
+    const bool full = span == TILE;
+    const uint64_t g = T.g;
+    const uint64_t probe = T.probe;
+    const v4u* v = T.v;
+    // Only a guess miss reads the probe.  Used on that path alone, the load
+    // would be sunk into it, behind the data loads (vector loads return in
+    // issue order: a ragged tile would wait for its data before searching),
+    // so every path ends with keep_probe(): a test that is never true for a
+    // batch the host launches (n > 0), after the tile's stores, where the
+    // probe is long back.
+    auto keep_probe = [&]() {
+        if (n == 0 && probe == ~uint64_t(0))
+            out[0] = 0;
+    };
+    TileLoc L;
+    locate(fs, n, g, stride, probe, base, L);
+    // frames touching the tile: a prefix of first, first + 1, ...
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k <= MAXF; ++k) {
+        const bool touches = uint64_t(L.first) + k < n && (k == 0 ? L.f0 >= 0 || L.st[0] < tend : L.st[k] < tend);
+        if (touches && c == k)
+            c = k + 1;
+    }
+
+    if (WSG_DIAG == 5 || (full && c <= MAXF)) {
+        // frames' payload segments in scalar registers (full tiles; the
+        // wire's last, partial tile takes the staged path)
+        Seg S[MAXF];
+#pragma unroll
+        for (int k = 0; k < MAXF; ++k) {
+            S[k] = Seg{0, 0, 0};
+            if (k < c) {
+                wsg_recv_info r;
+                const uint64_t lim = (uint64_t(L.first) + k + 1 < n) ? L.st[k + 1] : wire_len;
+                frame_parse(wire, wire_len, L.st[k], lim, r);
+                const Seg g = tile_seg(r.payload_off, r.payload_off + r.len, r.key, base, span);
+                S[k] = Seg{uni(g.lo), uni(g.hi), uni(g.kr)};
+            }
+        }
+#if WSG_DIAG == 5   // timing-only: every tile streams with its first frame's key (8-wave register budget)
+        if (true) {
+#else
+        if (S[0].lo == 0 && S[0].hi == TILE) {
+#endif
+            // stream: the whole tile is payload of one frame
+            const OutTile ot(out + base, uint32_t(TILE));
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u)
+                ot.put(uint32_t(lane_off(u)), v[u] ^ S[0].kr);
+            keep_probe();
+            return;
+        }
+        const OutTile ot(out + base, uint32_t(TILE));
+        // boundary: per chunk, the key word of the segment holding it;
+        // the few chunks a segment edge cuts build byte masks
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint32_t o = uint32_t(lane_off(u));
+            uint32_t kx = 0;
+            bool cut = false;
+#pragma unroll
+            for (int k = 0; k < MAXF; ++k) {
+                kx = (S[k].lo <= o && o + CHUNK <= S[k].hi) ? S[k].kr : kx;
+                cut |= (S[k].lo > o && S[k].lo < o + CHUNK) || (S[k].hi > o && S[k].hi < o + CHUNK);
+            }
+            v4u x = v4u{kx, kx, kx, kx};
+            if (cut) {
+                x = seg_xor(o, S[0]);
+#pragma unroll
+                for (int k = 1; k < MAXF; ++k)
+                    x |= seg_xor(o, S[k]);
+            }
+            ot.put(o, v[u] ^ x);
+        }
+        keep_probe();
+        return;
+    }
+
+    // staged: payload segments in LDS, LDSF frames per round
+    __shared__ uint32_t s_lo[LDSF], s_hi[LDSF], s_kr[LDSF];
+    __shared__ uint32_t s_wcnt[BLOCK / 64];
+    // stage the segments of frames r0, r0 + 1, ... that touch the tile;
+    // more = frames past the stage touch it too (block-uniform)
+    auto stage = [&](uint64_t r0, int& cnt, bool& more) {
+        // slot q * BLOCK + lane holds frame r0 + q * BLOCK + lane
+        uint64_t sj[SPL], lim[SPL];
+        bool touch[SPL];
+#pragma unroll
+        for (int q = 0; q < SPL; ++q) {
+            const uint64_t fi = r0 + uint64_t(q) * BLOCK + threadIdx.x;
+            sj[q] = ~uint64_t(0);
+            lim[q] = wire_len;
+            if (fi < n) {
+                sj[q] = fs[fi];
+                lim[q] = fi + 1 < n ? fs[fi + 1] : wire_len;
+            }
+            // frame `first` touches (c > MAXF); the others when they start in the tile
+            touch[q] = fi < n && (fi == L.first || sj[q] < tend);
+        }
+        // block-wide counts from wave ballots through LDS (the
+        // __syncthreads_count / _or builtins cost ~40 VGPRs here,
+        // tools/regs.py: 91 vs 53 for the whole kernel)
+        uint32_t wc = 0;
+#pragma unroll
+        for (int q = 0; q < SPL; ++q)
+            wc += uint32_t(__builtin_popcountll(__ballot(touch[q])));
+        const bool last_more = __ballot(threadIdx.x == BLOCK - 1 && touch[SPL - 1] &&
+                                        r0 + uint64_t(LDSF) < n && lim[SPL - 1] < tend) != 0;
+        __syncthreads();   // the previous readers are done with the stage and the counts
+        if ((threadIdx.x & 63) == 0)
+            s_wcnt[threadIdx.x >> 6] = wc | (last_more ? 0x80000000u : 0u);
+        __syncthreads();
+        cnt = 0;
+        more = false;
+#pragma unroll
+        for (int w = 0; w < BLOCK / 64; ++w) {
+            const uint32_t x = s_wcnt[w];
+            cnt += int(x & 0x7FFFFFFFu);
+            more = more || (x >> 31) != 0;
+        }
+#pragma unroll 1
+        for (int q = 0; q < SPL; ++q) {
+            const int slot = q * BLOCK + int(threadIdx.x);
+            if (slot < cnt) {
+                wsg_recv_info r;
+                frame_parse(wire, wire_len, sj[q], lim[q], r);
+                const Seg g = tile_seg(r.payload_off, r.payload_off + r.len, r.key, base, span);
+                s_lo[slot] = g.lo;
+                s_hi[slot] = g.hi;
+                s_kr[slot] = g.kr;
+            }
+        }
+        __syncthreads();
+    };
+    // XOR words of the staged segments for the chunk at tile offset o
+    auto chunk_xor = [&](uint32_t o, int cnt) {
+        int lo = 0, hi = cnt;   // first segment ending after o (segment ends are non-decreasing)
+#pragma unroll 1
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_hi[mid] <= o)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        v4u x = {0, 0, 0, 0};
+#pragma unroll 1
+        for (int j = lo; j < cnt && s_lo[j] < o + CHUNK; ++j)
+            x |= seg_xor(o, Seg{s_lo[j], s_hi[j], s_kr[j]});
+        return x;
+    };
+    // rounds of LDSF frames (one for every tile but those of the tiniest
+    // frames): each round ORs its segments' XOR words into the thread's
+    // own LDS slots, then one pass reads the tile's bytes again (L2 /
+    // Infinity-Cache warm), XORs and stores.  Nothing is carried in
+    // registers across the staging: this path would otherwise set the
+    // kernel's register budget (95 VGPRs with the tile held in registers
+    // and a per-round store, 5 waves/SIMD; tools/regs.py).
+    __shared__ v4u s_acc[UNROLL][BLOCK];
+#pragma unroll 1
+    for (uint64_t r0 = L.first;; r0 += LDSF) {
+        int cnt;
+        bool more;
+        stage(r0, cnt, more);
+#pragma unroll 1
+        for (int u = 0; u < UNROLL; ++u) {
+            const v4u x = chunk_xor(uint32_t(lane_off(u)), cnt);
+            s_acc[u][threadIdx.x] = (r0 == L.first) ? x : (s_acc[u][threadIdx.x] | x);
+        }
+        if (!more)
+            break;
+    }
+    {
+        const OutTile ot(out + base, uint32_t(TILE));
+#pragma unroll 1
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint32_t o = uint32_t(lane_off(u));
+            if (o + CHUNK <= span) {
+                ot.put(o, ld16(wire + base + o) ^ s_acc[u][threadIdx.x]);
+            } else if (o < span) {
+                // the chunk the wire's end cuts: bytes only, through the
+                // thread's LDS slot (no register byte shuffles)
+                uint8_t* b = reinterpret_cast<uint8_t*>(&s_acc[u][threadIdx.x]);
+#pragma unroll 1
+                for (uint32_t k = 0; k < span - o; ++k)
+                    out[base + o + k] = uint8_t(wire[base + o + k] ^ b[k]);
+            }
+        }
+    }
+    keep_probe();
+}
+
 } // namespace
 
 // Decode (ws.cpp:320-406 over a batch): out = wire with every payload XORed
@@ -528,224 +765,25 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
     }
     return;
 #endif
-    for (uint64_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
-        const uint64_t base = t * TILE;
-        const uint64_t tend = min(base + TILE, wire_len);
-        const uint32_t span = uint32_t(tend - base);
-        const bool full = span == TILE;
-
-        // coarse probe of the frame table (vector load, issued before the
-        // data loads: loads return in issue order)
-        const uint64_t g = tile_guess(n, frames_per_byte, base);
-#if WSG_DIAG == 7   // timing-only: no coarse probe (right only where the guess is exact: equal-size frames)
-        uint64_t probe = 0;
-#else
-        const uint64_t probe = fs[probe_index(g, stride, n, int(threadIdx.x & 63))];
-#endif
-        // Only a guess miss reads the probe.  Used on that path alone, the
-        // load would be sunk into it, behind the data loads (vector loads
-        // return in issue order: a ragged tile would wait for its data
-        // before searching), so every path ends with keep_probe(): a test
-        // that is never true for a batch the host launches (n > 0), after
-        // the tile's stores, where the probe is long back.
-        auto keep_probe = [&]() {
-            if (n == 0 && probe == ~uint64_t(0))
-                out[0] = 0;
-        };
-        __builtin_amdgcn_sched_barrier(0);
-
-        // the tile's data does not depend on frame metadata: issue it next,
-        // unconditionally, so that the metadata chain below waits for the
-        // probe alone (vmcnt(UNROLL)); loads behind a branch made the compiler
-        // wait vmcnt(0) there, i.e. start the chain only once the whole tile
-        // had arrived.  The wire's last, partial tile takes the staged path,
-        // which reads its bytes itself: its loads here are clamped to the
-        // 16-B block holding the last wire byte (readable by contract) and
-        // their values are not used.
-        const uint64_t last_blk = (wire_len - 1) & ~uint64_t(CHUNK - 1);
-        v4u v[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u)
-            v[u] = ld16nt(wire + min(base + lane_off(u), last_blk));
-
-        TileLoc L;
-        locate(fs, n, g, stride, probe, base, L);
-        // frames touching the tile: a prefix of first, first + 1, ...
-        int c = 0;
-#pragma unroll
-        for (int k = 0; k <= MAXF; ++k) {
-            const bool touches = uint64_t(L.first) + k < n && (k == 0 ? L.f0 >= 0 || L.st[0] < tend : L.st[k] < tend);
-            if (touches && c == k)
-                c = k + 1;
-        }
-
-        if (WSG_DIAG == 5 || (full && c <= MAXF)) {
-            // frames' payload segments in scalar registers (full tiles; the
-            // wire's last, partial tile takes the staged path)
-            Seg S[MAXF];
-#pragma unroll
-            for (int k = 0; k < MAXF; ++k) {
-                S[k] = Seg{0, 0, 0};
-                if (k < c) {
-                    wsg_recv_info r;
-                    const uint64_t lim = (uint64_t(L.first) + k + 1 < n) ? L.st[k + 1] : wire_len;
-                    frame_parse(wire, wire_len, L.st[k], lim, r);
-                    const Seg g = tile_seg(r.payload_off, r.payload_off + r.len, r.key, base, span);
-                    S[k] = Seg{uni(g.lo), uni(g.hi), uni(g.kr)};
-                }
-            }
-#if WSG_DIAG == 5   // timing-only: every tile streams with its first frame's key (8-wave register budget)
-            if (true) {
-#else
-            if (S[0].lo == 0 && S[0].hi == TILE) {
-#endif
-                // stream: the whole tile is payload of one frame
-                const OutTile ot(out + base, uint32_t(TILE));
-#pragma unroll
-                for (int u = 0; u < UNROLL; ++u)
-                    ot.put(uint32_t(lane_off(u)), v[u] ^ S[0].kr);
-                keep_probe();
-                continue;
-            }
-            const OutTile ot(out + base, uint32_t(TILE));
-            // boundary: per chunk, the key word of the segment holding it;
-            // the few chunks a segment edge cuts build byte masks
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const uint32_t o = uint32_t(lane_off(u));
-                uint32_t kx = 0;
-                bool cut = false;
-#pragma unroll
-                for (int k = 0; k < MAXF; ++k) {
-                    kx = (S[k].lo <= o && o + CHUNK <= S[k].hi) ? S[k].kr : kx;
-                    cut |= (S[k].lo > o && S[k].lo < o + CHUNK) || (S[k].hi > o && S[k].hi < o + CHUNK);
-                }
-                v4u x = v4u{kx, kx, kx, kx};
-                if (cut) {
-                    x = seg_xor(o, S[0]);
-#pragma unroll
-                    for (int k = 1; k < MAXF; ++k)
-                        x |= seg_xor(o, S[k]);
-                }
-                ot.put(o, v[u] ^ x);
-            }
-            keep_probe();
-            continue;
-        }
-
-        // staged: payload segments in LDS, LDSF frames per round
-        __shared__ uint32_t s_lo[LDSF], s_hi[LDSF], s_kr[LDSF];
-        __shared__ uint32_t s_wcnt[BLOCK / 64];
-        // stage the segments of frames r0, r0 + 1, ... that touch the tile;
-        // more = frames past the stage touch it too (block-uniform)
-        auto stage = [&](uint64_t r0, int& cnt, bool& more) {
-            // slot q * BLOCK + lane holds frame r0 + q * BLOCK + lane
-            uint64_t sj[SPL], lim[SPL];
-            bool touch[SPL];
-#pragma unroll
-            for (int q = 0; q < SPL; ++q) {
-                const uint64_t fi = r0 + uint64_t(q) * BLOCK + threadIdx.x;
-                sj[q] = ~uint64_t(0);
-                lim[q] = wire_len;
-                if (fi < n) {
-                    sj[q] = fs[fi];
-                    lim[q] = fi + 1 < n ? fs[fi + 1] : wire_len;
-                }
-                // frame `first` touches (c > MAXF); the others when they start in the tile
-                touch[q] = fi < n && (fi == L.first || sj[q] < tend);
-            }
-            // block-wide counts from wave ballots through LDS (the
-            // __syncthreads_count / _or builtins cost ~40 VGPRs here,
-            // tools/regs.py: 91 vs 53 for the whole kernel)
-            uint32_t wc = 0;
-#pragma unroll
-            for (int q = 0; q < SPL; ++q)
-                wc += uint32_t(__builtin_popcountll(__ballot(touch[q])));
-            const bool last_more = __ballot(threadIdx.x == BLOCK - 1 && touch[SPL - 1] &&
-                                            r0 + uint64_t(LDSF) < n && lim[SPL - 1] < tend) != 0;
-            __syncthreads();   // the previous readers are done with the stage and the counts
-            if ((threadIdx.x & 63) == 0)
-                s_wcnt[threadIdx.x >> 6] = wc | (last_more ? 0x80000000u : 0u);
-            __syncthreads();
-            cnt = 0;
-            more = false;
-#pragma unroll
-            for (int w = 0; w < BLOCK / 64; ++w) {
-                const uint32_t x = s_wcnt[w];
-                cnt += int(x & 0x7FFFFFFFu);
-                more = more || (x >> 31) != 0;
-            }
-#pragma unroll 1
-            for (int q = 0; q < SPL; ++q) {
-                const int slot = q * BLOCK + int(threadIdx.x);
-                if (slot < cnt) {
-                    wsg_recv_info r;
-                    frame_parse(wire, wire_len, sj[q], lim[q], r);
-                    const Seg g = tile_seg(r.payload_off, r.payload_off + r.len, r.key, base, span);
-                    s_lo[slot] = g.lo;
-                    s_hi[slot] = g.hi;
-                    s_kr[slot] = g.kr;
-                }
-            }
-            __syncthreads();
-        };
-        // XOR words of the staged segments for the chunk at tile offset o
-        auto chunk_xor = [&](uint32_t o, int cnt) {
-            int lo = 0, hi = cnt;   // first segment ending after o (segment ends are non-decreasing)
-#pragma unroll 1
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (s_hi[mid] <= o)
-                    lo = mid + 1;
-                else
-                    hi = mid;
-            }
-            v4u x = {0, 0, 0, 0};
-#pragma unroll 1
-            for (int j = lo; j < cnt && s_lo[j] < o + CHUNK; ++j)
-                x |= seg_xor(o, Seg{s_lo[j], s_hi[j], s_kr[j]});
-            return x;
-        };
-        // rounds of LDSF frames (one for every tile but those of the tiniest
-        // frames): each round ORs its segments' XOR words into the thread's
-        // own LDS slots, then one pass reads the tile's bytes again (L2 /
-        // Infinity-Cache warm), XORs and stores.  Nothing is carried in
-        // registers across the staging: this path would otherwise set the
-        // kernel's register budget (95 VGPRs with the tile held in registers
-        // and a per-round store, 5 waves/SIMD; tools/regs.py).
-        __shared__ v4u s_acc[UNROLL][BLOCK];
-#pragma unroll 1
-        for (uint64_t r0 = L.first;; r0 += LDSF) {
-            int cnt;
-            bool more;
-            stage(r0, cnt, more);
-#pragma unroll 1
-            for (int u = 0; u < UNROLL; ++u) {
-                const v4u x = chunk_xor(uint32_t(lane_off(u)), cnt);
-                s_acc[u][threadIdx.x] = (r0 == L.first) ? x : (s_acc[u][threadIdx.x] | x);
-            }
-            if (!more)
-                break;
-        }
-        {
-            const OutTile ot(out + base, uint32_t(TILE));
-#pragma unroll 1
-            for (int u = 0; u < UNROLL; ++u) {
-                const uint32_t o = uint32_t(lane_off(u));
-                if (o + CHUNK <= span) {
-                    ot.put(o, ld16(wire + base + o) ^ s_acc[u][threadIdx.x]);
-                } else if (o < span) {
-                    // the chunk the wire's end cuts: bytes only, through the
-                    // thread's LDS slot (no register byte shuffles)
-                    uint8_t* b = reinterpret_cast<uint8_t*>(&s_acc[u][threadIdx.x]);
-#pragma unroll 1
-                    for (uint32_t k = 0; k < span - o; ++k)
-                        out[base + o + k] = uint8_t(wire[base + o + k] ^ b[k]);
-                }
-            }
-        }
-        keep_probe();
+#if WSG_DEC_PAIR
+    // two tiles per block, both tiles' loads in flight before the first
+    // tile's metadata chain (separate registers: the second tile's loads do
+    // not wait for the first one's stores); host grid: ceil(tiles / 2)
+    for (uint64_t t = 2 * uint64_t(blockIdx.x); t < num_tiles; t += 2 * uint64_t(gridDim.x)) {
+        TileIn a, b;
+        load_tile(a, wire, wire_len, fs, n, frames_per_byte, stride, t * TILE);
+        load_tile(b, wire, wire_len, fs, n, frames_per_byte, stride, min(t + 1, num_tiles - 1) * TILE);
+        process_tile(a, wire, out, wire_len, fs, n, stride);
+        if (t + 1 < num_tiles)
+            process_tile(b, wire, out, wire_len, fs, n, stride);
     }
+#else
+    for (uint64_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
+        TileIn a;
+        load_tile(a, wire, wire_len, fs, n, frames_per_byte, stride, t * TILE);
+        process_tile(a, wire, out, wire_len, fs, n, stride);
+    }
+#endif
     if (WSG_DEC_INFO_LAST)
         info_slice();
 }
