@@ -748,6 +748,57 @@ def c5_job_leg(world, rank, device, codec, n_total=1 << 20, size=16384, chunk=10
     return res
 
 
+def pcie_all_ranks_leg(w, world, rank, device, reps=3):
+    """The host-inclusive decode (pinned host wire -> H2D -> k_decode -> D2H,
+    wsg_decode_batch_host) on every rank at once, each over its own GPU's
+    PCIe link: the one-process-per-GPU form of a server decoding socket
+    buffers on all GPUs.  Payload GiB/s over all ranks (max-over-ranks time)
+    and one rank's own rate."""
+    import cppserver_amd as ca
+
+    # every rank reaches every collective below, whatever fails locally (a
+    # rank that raised between them would leave the others waiting)
+    wire, fs, _ = w.host
+    err = None
+    try:
+        pin_in, pin_out = ca.pinned_empty(len(wire)), ca.pinned_empty(len(wire))
+        pin_in[:] = wire
+        rc, _, _ = w.codec.decode_batch_host(pin_in, fs, out=pin_out)   # warm (staging slots)
+        if rc != 0:
+            err = "wsg_decode_batch_host: %d" % rc
+    except Exception as e:   # noqa: BLE001
+        err = repr(e)[:200]
+    barrier(world)
+    t0 = time.perf_counter()
+    if err is None:
+        for _ in range(reps):
+            rc, _, _ = w.codec.decode_batch_host(pin_in, fs, out=pin_out)
+            if rc != 0:
+                err = "wsg_decode_batch_host: %d" % rc
+                break
+    dt = time.perf_counter() - t0 if err is None else float("inf")
+    mine = w.payload_bytes * reps / dt / GIB
+    dt = max_over_ranks(dt, world, device)
+    if err is not None or dt == float("inf"):
+        return {"error": err or "another rank failed"}
+    ok = bool(np.array_equal(pin_out[int(fs[0]): int(fs[0]) + 64], np.asarray(oracle_decode_head(wire, fs))))
+    return {"workload": "every rank: %d x %d B frames from pinned host memory, decoded on its GPU"
+                        % (len(fs), w.payload_bytes // len(fs)),
+            "all_ranks_GiBps": round(world * w.payload_bytes * reps / dt / GIB, 2),
+            "rank0_GiBps": round(mine, 2), "check": ok}
+
+
+def oracle_decode_head(wire, fs):
+    """The first 64 output bytes of frame 0 (the oracle's decode of it)."""
+    import oracle
+
+    a = int(fs[0])
+    b = int(fs[1]) if len(fs) > 1 else len(wire)
+    rc, ref, _ = oracle.decode_batch(np.ascontiguousarray(wire[a:b]), np.zeros(1, np.uint64))
+    assert rc == 0
+    return ref[:64]
+
+
 def c5_capi_leg(world, rank, n_total=1 << 20, timeout=300):
     """C5 through the one-process multi-GPU C-ABI entry (SURVEY §8b-3:
     wsg_mgpu_create over all N GPUs, RCCL inside the library), what a C++
@@ -862,6 +913,11 @@ def main():
     extras = {}
     if w.cfg == "c5" and world > 1:
         extras["gather"] = gather_leg(w, world, rank, device)
+    if w.cfg == "c2" and world > 1 and not args.no_extras:
+        try:
+            extras["pcie_inclusive_all_ranks"] = pcie_all_ranks_leg(w, world, rank, device)
+        except Exception as e:   # noqa: BLE001  (reported; the headline stands)
+            extras["pcie_inclusive_all_ranks"] = {"error": repr(e)[:300]}
     if w.cfg == "c2" and world > 1 and not args.no_c5_job:
         # C5 (BASELINE configs[4]) on the same GPUs: a failure here is reported
         # in the line, it does not take the headline with it
