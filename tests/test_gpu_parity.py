@@ -608,3 +608,109 @@ def test_timing_hook_counts_launches(codec):
     codec.timing(False)
     codec.sync()
     assert launches == 3 and ms > 0
+
+
+def _xor_key_chunks(x, key, at):
+    """x ^ key bytes (byte j of the key = (key >> 8j) & 0xFF) for a chunk of
+    payload that starts at payload offset `at` (a multiple of 4)."""
+    kb = torch.tensor(list(int(key).to_bytes(4, "little")), dtype=torch.uint8, device=x.device)
+    reps = (x.numel() + 3) // 4
+    return x ^ kb.repeat(reps)[: x.numel()]
+
+
+@pytest.mark.parametrize("length", [(5 << 30) + 3])
+def test_single_frame_over_4gib(codec, length):
+    """Maximum sizes: ONE frame whose payload passes 2^32 bytes (64-bit length
+    header, ws.cpp:234-239 / :354-371; every 64-bit offset in the kernels
+    past the u32 range).  Encode: the header equals wsg_header_pack's (the
+    host code the KAT vectors pin) and the payload is x ^ key (ws.cpp:269-270,
+    key byte i % 4), checked in 1 GiB chunks on the device; decode of the
+    encoded wire, out of place and in place, gives the payload back with the
+    frame's fields; the encoded first and last MiB also byte for byte
+    against the oracle."""
+    key = 0xA1B2C3D4
+    gen = torch.Generator(device="cuda").manual_seed(4242)
+    payload = torch.randint(0, 256, (length,), dtype=torch.uint8, device="cuda", generator=gen)
+    desc = np.zeros(1, dtype=SEND_DESC)
+    desc["len"], desc["key"], desc["opcode"], desc["mask"] = length, key, 0x82, 1
+    hdr = ca.header_pack(0x82, True, length, 0, key)
+    assert len(hdr) == 14
+    wire, off = codec.encode_batch(payload, ca.desc_to_tensor(desc, "cuda"), wire_cap=length + 14)
+    assert codec.sync_status() == 0
+    assert int(off[1].item()) == length + 14
+    assert bytes(wire[:14].cpu().numpy()) == hdr
+    step = 1 << 30
+    for a in range(0, length, step):
+        b = min(a + step, length)
+        assert torch.equal(wire[14 + a: 14 + b], _xor_key_chunks(payload[a:b], key, a)), "encode chunk %d" % a
+    # the GPU's encoded bytes around the payload's first and last MiB against
+    # the oracle's encode of a frame of the same header class (64-bit
+    # length) over those bytes (key phase 0 at a multiple of 4)
+    for a in (0, length - (1 << 20)):
+        a -= a % 4
+        part = payload[a: a + (1 << 20)].cpu().numpy()
+        d = desc.copy()
+        d["len"] = len(part)
+        w_o, _ = oracle.encode_batch(part, d)
+        assert np.array_equal(wire[14 + a: 14 + a + len(part)].cpu().numpy(), w_o[14:]), "oracle at %d" % a
+    fs = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out, info = codec.decode_batch(wire, fs)
+    assert codec.sync_status() == 0
+    r = ca.info_to_numpy(info, 1)[0]
+    assert (int(r["payload_off"]), int(r["len"]), int(r["key"]), int(r["opcode"]), int(r["fin"]), int(r["error"])) \
+        == (14, length, key, 2, 1, 0)
+    for a in range(0, length, step):
+        b = min(a + step, length)
+        assert torch.equal(out[14 + a: 14 + b], payload[a:b]), "decode chunk %d" % a
+    del out
+    codec.decode_batch(wire, fs, out=wire)   # in place
+    assert codec.sync_status() == 0
+    for a in range(0, length, step):
+        b = min(a + step, length)
+        assert torch.equal(wire[14 + a: 14 + b], payload[a:b]), "in-place chunk %d" % a
+    del payload, wire
+
+
+def test_ragged_wire_over_4gib(codec):
+    """Maximum sizes, many frames: a 90,000-frame ragged batch (payload 0 to
+    110,000 B, ~4.95 GB of wire) encoded and decoded on the GPU, so frame
+    starts, tiles and payloads straddle the 2^32-byte mark.  Every frame's
+    decode info vs its descriptor (vectorized); payloads of the frames around
+    2^32 and 500 sampled ones vs their input; the wire around 2^32 decoded
+    byte for byte by the oracle."""
+    rng = np.random.default_rng(432)
+    n = 90000
+    lens = rng.integers(0, 110001, n).astype(np.uint64)
+    desc = np.zeros(n, dtype=SEND_DESC)
+    desc["len"] = lens
+    desc["src_off"][1:] = np.cumsum(lens)[:-1]
+    desc["key"] = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    desc["opcode"], desc["mask"] = 0x82, 1
+    total = int(lens.sum())
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    payload = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda", generator=gen)
+    sizes = ca.frame_sizes(desc).astype(np.uint64)
+    cap = int(sizes.sum())
+    assert cap > (1 << 32) + (1 << 28)
+    wire, off = codec.encode_batch(payload, ca.desc_to_tensor(desc, "cuda"), wire_cap=cap)
+    assert codec.sync_status() == 0
+    offs = off.cpu().numpy().view(np.uint64)
+    assert np.array_equal(offs[1:], np.cumsum(sizes))
+    out, info = codec.decode_batch(wire, off[:-1])
+    assert codec.sync_status() == 0
+    r = ca.info_to_numpy(info, n)
+    hdr = sizes - lens
+    assert np.array_equal(r["payload_off"], offs[:-1] + hdr)
+    assert np.array_equal(r["len"], lens)
+    assert np.array_equal(r["key"], desc["key"])
+    assert not r["error"].any()
+    j = int(np.searchsorted(offs, 1 << 32, side="right")) - 1   # the frame holding byte 2^32
+    pick = sorted(set(range(max(0, j - 20), min(n, j + 21))) | set(rng.integers(0, n, 500).tolist()))
+    for i in pick:
+        po, ln, so = int(r["payload_off"][i]), int(lens[i]), int(desc["src_off"][i])
+        assert torch.equal(out[po: po + ln], payload[so: so + ln]), "frame %d" % i
+    a, b = max(0, j - 5), min(n, j + 6)
+    lo, hi = int(offs[a]), int(offs[b])
+    rc_o, out_o, _ = oracle.decode_batch(wire[lo:hi].cpu().numpy(), (offs[a:b] - offs[a]).astype(np.uint64))
+    assert rc_o == 0 and np.array_equal(out[lo:hi].cpu().numpy(), out_o)
+    del payload, wire, out
