@@ -714,3 +714,32 @@ def test_ragged_wire_over_4gib(codec):
     rc_o, out_o, _ = oracle.decode_batch(wire[lo:hi].cpu().numpy(), (offs[a:b] - offs[a]).astype(np.uint64))
     assert rc_o == 0 and np.array_equal(out[lo:hi].cpu().numpy(), out_o)
     del payload, wire, out
+
+
+def test_host_pipeline_frames_larger_than_segments(codec, monkeypatch):
+    """The host-staged paths cut batches into ~$WSG_STAGE_MB segments of whole
+    frames; frames several times a segment's size make segments of one frame
+    each (decode and encode, pinned and pageable) and still match the oracle."""
+    monkeypatch.setenv("WSG_STAGE_MB", "1")
+    rng = np.random.default_rng(77)
+    lens = np.array([5 << 20, 17, (3 << 20) + 5, 0, 2 << 20], dtype=np.uint64)
+    payload = wl.random_bytes(rng, int(lens.sum()) + 16)
+    desc = np.zeros(len(lens), dtype=SEND_DESC)
+    desc["len"] = lens
+    desc["src_off"][1:] = np.cumsum(lens)[:-1]
+    desc["key"] = rng.integers(1, 2**32, len(lens), dtype=np.uint64).astype(np.uint32)
+    desc["opcode"], desc["mask"] = 0x82, 1
+    wire_o, off_o = oracle.encode_batch(payload, desc)
+    rc_o, out_o, info_o = oracle.decode_batch(wire_o, off_o[:-1])
+    assert rc_o == 0
+    for pinned in (False, True):
+        p = payload
+        if pinned:
+            p = ca.pinned_empty(len(payload))
+            p[:] = payload
+        rc, wire, off = codec.encode_batch_host(p, desc)
+        assert rc == 0 and np.array_equal(wire, wire_o) and np.array_equal(off, off_o)
+        rc, out, info = codec.decode_batch_host(wire_o, off_o[:-1])
+        assert rc == 0 and np.array_equal(out, out_o)
+        for f in INFO_FIELDS:
+            assert np.array_equal(info[f], info_o[f]), f
