@@ -225,6 +225,26 @@ class Codec:
         _check(rc, "wsg_decode_batch")
         return out, info
 
+    def prepare_decode(self, wire, frame_start, out, info, stream=None):
+        """wsg_decode_batch on fixed buffers (a server's batch arena), with
+        the ctypes arguments bound once: returns a callable that launches one
+        decode per call (asynchronous, like decode_batch)."""
+        n = int(frame_start.numel())
+        assert int(out.numel()) >= int(wire.numel()) and int(info.numel()) >= n * RECV_INFO.itemsize
+        fn, st = self._L.wsg_decode_batch, self._stream(stream)
+        args = (self._ctx, ctypes.c_void_p(wire.data_ptr()), ctypes.c_uint64(wire.numel()),
+                ctypes.c_void_p(frame_start.data_ptr()), ctypes.c_uint32(n), ctypes.c_void_p(out.data_ptr()),
+                ctypes.c_void_p(info.data_ptr()), st)
+        keep = (wire, frame_start, out, info)   # the buffers live as long as the callable
+
+        def launch():
+            rc = fn(*args)
+            if rc != 0:
+                raise WSGError(rc, "wsg_decode_batch")
+            return keep
+
+        return launch
+
     # -- batch encode (mask) --------------------------------------------------
     def encode_batch(self, payload, desc, wire=None, wire_cap=None, wire_off=None, stream=None):
         """Encode frames ``desc`` (uint8 CUDA tensor of n*32 bytes) whose data

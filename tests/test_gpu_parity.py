@@ -743,3 +743,22 @@ def test_host_pipeline_frames_larger_than_segments(codec, monkeypatch):
         assert rc == 0 and np.array_equal(out, out_o)
         for f in INFO_FIELDS:
             assert np.array_equal(info[f], info_o[f]), f
+
+
+def test_prepare_decode_matches_decode_batch(codec):
+    """Codec.prepare_decode (the bench's pre-bound C-ABI launch) decodes the
+    same bytes and fields as decode_batch, launch after launch."""
+    wire, fs, _ = wl.c2_wire(64, 5000, seed=12)
+    w = dev(wire)
+    f = dev(fs.view(np.int64))
+    out = torch.empty_like(w)
+    info = torch.empty(64 * RECV_INFO.itemsize, dtype=torch.uint8, device="cuda")
+    launch = codec.prepare_decode(w, f, out, info)
+    for _ in range(3):
+        launch()
+    assert codec.sync_status() == 0
+    rc, out_r, info_r = gpu_decode(codec, wire, fs)
+    assert rc == 0 and np.array_equal(out.cpu().numpy(), out_r)
+    got = ca.info_to_numpy(info, 64)
+    for fld in INFO_FIELDS:
+        assert np.array_equal(got[fld], info_r[fld]), fld
