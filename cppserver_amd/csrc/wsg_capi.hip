@@ -3,6 +3,7 @@
 // Nothing here computes payload bytes on the CPU: every payload byte of
 // every entry point is produced by a gfx950 kernel.
 #include "wsg_internal.h"
+#include "wsg_trace.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -592,6 +593,7 @@ int wsg_fanout_encode_many(wsg_ctx* c, const uint8_t* d_payload, const uint64_t*
 
 int wsg_xor_host(wsg_ctx* c, const void* src, void* dst, size_t len, uint32_t key, uint32_t phase)
 {
+    const wsg::TraceRange trace_range("wsg.xor_host");
     if (!c || (len && (!src || !dst)))
         return WSG_EINVAL;
     if (len == 0)
@@ -760,6 +762,7 @@ int wsg_host_free(void* p)
 int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start,
                           uint32_t n, uint8_t* out, wsg_recv_info* info)
 {
+    const wsg::TraceRange trace_range("wsg.decode_batch_host");
     try {   // no C++ exception leaves the ABI (host vectors: WSG_ENOMEM)
         if (!c || (wire_len && (!wire || !out)) || (n && (!frame_start || !info)))
             return WSG_EINVAL;
@@ -922,6 +925,7 @@ int slot_reserve_enc(wsg_ctx::Slot& sl, uint64_t payload_bytes, uint64_t wire_by
 int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_len, const wsg_send_desc* desc,
                           uint32_t n, uint8_t* wire, uint64_t wire_cap, uint64_t* wire_off)
 {
+    const wsg::TraceRange trace_range("wsg.encode_batch_host");
     try {   // no C++ exception leaves the ABI (host vectors: WSG_ENOMEM)
         if (!c || !wire_off || (n && (!desc || !wire)) || (payload_len && !payload))
             return WSG_EINVAL;

@@ -24,6 +24,7 @@
 // ROCm install, so that a host process which already carries another RCCL
 // (PyTorch bundles one) keeps the two apart.
 #include "wsg_internal.h"
+#include "wsg_trace.h"
 
 #include <rccl/rccl.h>
 
@@ -589,6 +590,7 @@ int wsg_mgpu_encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const 
                            const uint64_t* wire_cap, uint64_t* const* d_wire_off, int root, uint8_t* d_out,
                            uint64_t out_cap, uint64_t* d_out_off, double* times)
 {
+    const wsg::TraceRange trace_range("wsg.mgpu_encode_gather");
     try {   // no C++ exception leaves the ABI (host vectors: WSG_ENOMEM)
         return encode_gather(g, n_total, chunk, d_payload, d_desc, n_local, d_wire, wire_cap, d_wire_off, root, d_out,
                              out_cap, d_out_off, times);
@@ -719,6 +721,7 @@ extern "C" {
 int wsg_decode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* wire, uint64_t wire_len,
                                 const uint64_t* frame_start, uint32_t n, uint8_t* out, wsg_recv_info* info)
 {
+    const wsg::TraceRange trace_range("wsg.decode_batch_host_multi");
     try {
         return decode_host_multi(ctxs, nctx, wire, wire_len, frame_start, n, out, info);
     } catch (...) {
@@ -730,6 +733,7 @@ int wsg_encode_batch_host_multi(wsg_ctx* const* ctxs, int nctx, const uint8_t* p
                                 const wsg_send_desc* desc, uint32_t n, uint8_t* wire, uint64_t wire_cap,
                                 uint64_t* wire_off)
 {
+    const wsg::TraceRange trace_range("wsg.encode_batch_host_multi");
     try {
         return encode_host_multi(ctxs, nctx, payload, payload_len, desc, n, wire, wire_cap, wire_off);
     } catch (...) {

@@ -16,5 +16,5 @@ $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws_api.cpp -
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws_batch.cpp -o b.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/http.cpp -o h.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/wsg_mgpu.cpp -o m.o
-$H --offload-arch=gfx950 -shared -o libwsg.so k.o c.o w.o a.o b.o h.o m.o -lcrypto -ldl
+$H --offload-arch=gfx950 -shared -o libwsg.so k.o c.o w.o a.o b.o h.o m.o -lcrypto -ldl -L/opt/rocm/lib -lrocprofiler-sdk-roctx
 echo "$out/libwsg.so"
