@@ -30,6 +30,7 @@ struct wsg_ctx {
     int enc_blocks_per_cu = 1024; // k_encode_mask grid, ~1-2 pieces per wave (tools/tune_enc.py: C5 share -15 %, C3-like -6 % vs 32)
     uint64_t xor_direct_max = 64 << 10;   // per-call XOR: kernel on the pinned stage up to this size (A/B: $WSG_XOR_DIRECT_MAX)
     int dec_tiles_per_block = 0;   // 0: grid from dec_blocks_per_cu alone; k: ceil(tiles / k) blocks (A/B)
+    bool check = false;            // $WSG_CHECK=1: operand ranges validated before every device launch (debug)
     int dec_blocks_per_cu = 4096;  // k_decode grid cap: one 16 KiB tile per block up to 16 GiB of wire (tools/tune.py, round 2: C2 84.3 vs 85.1 us at 48 blocks/CU, 88.1 at two tiles per block; C3 ragged 0.685 vs 0.705 ms at 256, 0.783 at 48)
     int fan_waves_per_cu = 8;    // fan-out period path: waves per CU (tools/tune_enc.py CFG=c4: 8 best of 4-32)
     uint64_t small_avg = wsg::SMALL_AVG;   // batch encode: k_encode_small when wire_cap <= n * small_avg
@@ -221,6 +222,27 @@ int drain_timing(wsg_ctx* c)
 
 int wsg::ctx_device(const wsg_ctx* c) { return c ? c->device : 0; }
 
+namespace {
+
+// Checked launches ($WSG_CHECK=1, a debug mode): [p, p + bytes) must lie in
+// ONE device allocation (hipMemGetAddressRange), which every access of the
+// kernel to that operand stays inside when the sizes passed are right.  GPU
+// address sanitizers are not available on the target pool; this catches a
+// short buffer or a wrong size on the host, before the kernel runs.
+bool in_alloc(const void* p, uint64_t bytes)
+{
+    if (bytes == 0)
+        return true;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) != hipSuccess)
+        return false;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p), b = reinterpret_cast<uintptr_t>(base);
+    return a >= b && a - b <= size && bytes <= size - (a - b);
+}
+
+} // namespace
+
 extern "C" {
 
 int wsg_abi_version(void) { return WSG_ABI_VERSION; }
@@ -279,6 +301,8 @@ int wsg_create(int device, wsg_ctx** out)
         if (v >= 0 && v <= 64)
             c->dec_tiles_per_block = v;
     }
+    if (const char* e = std::getenv("WSG_CHECK"))   // debug: checked launches (see in_alloc)
+        c->check = *e == '1';
     if (const char* e = std::getenv("WSG_ENC_BLOCKS_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
         const int v = std::atoi(e);
         if (v > 0 && v <= 4096)
@@ -407,6 +431,9 @@ int wsg_decode_batch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const
         return WSG_EINVAL;
     if (!aligned16(d_wire) || !aligned16(d_out))
         return WSG_EINVAL;
+    if (c->check && (!in_alloc(d_wire, (wire_len + 15) & ~uint64_t(15)) || !in_alloc(d_out, wire_len) ||
+                     !in_alloc(d_frame_start, uint64_t(n) * 8) || !in_alloc(d_info, uint64_t(n) * sizeof(wsg_recv_info))))
+        return WSG_EINVAL;
     return decode_launch(c, d_wire, wire_len, d_frame_start, n, d_out, d_info, pick(c, stream), c->d_err);
 }
 
@@ -466,6 +493,22 @@ int wsg_encode_batch(wsg_ctx* c, const uint8_t* d_payload, const wsg_send_desc* 
     if (n == 0) {
         WSG_HIP(hipMemsetAsync(d_wire_off, 0, sizeof(uint64_t), s));
         return WSG_OK;
+    }
+    if (c->check) {   // the descriptors come to the host: every payload range and the wire capacity
+        if (!in_alloc(d_desc, uint64_t(n) * sizeof(wsg_send_desc)) || !in_alloc(d_wire, wire_cap) ||
+            !in_alloc(d_wire_off, (uint64_t(n) + 1) * 8))
+            return WSG_EINVAL;
+        std::vector<wsg_send_desc> h;
+        try {
+            h.resize(n);
+        } catch (...) {
+            return WSG_ENOMEM;
+        }
+        WSG_HIP(hipMemcpyAsync(h.data(), d_desc, uint64_t(n) * sizeof(wsg_send_desc), hipMemcpyDeviceToHost, s));
+        WSG_HIP(hipStreamSynchronize(s));
+        for (const wsg_send_desc& d : h)
+            if (d.len && (!d_payload || !in_alloc(d_payload + d.src_off, d.len)))
+                return WSG_EINVAL;
     }
     if (int rc = ensure_enc(c, c->enc, n, wire_cap))
         return rc;
@@ -546,6 +589,8 @@ int wsg_fanout_encode(wsg_ctx* c, const uint8_t* d_payload, uint64_t len, const 
     const uint64_t total = wsg_frame_size(opcode, mask, len, 0) * k;
     if (total > wire_cap)
         return WSG_ENOMEM;
+    if (c->check && (!in_alloc(d_payload, len) || !in_alloc(d_keys, uint64_t(k) * 4) || !in_alloc(d_wire, total)))
+        return WSG_EINVAL;
     hipStream_t s = pick(c, stream);
     const uint64_t src = 0, off[2] = {0, total};
     const int t = timing_begin(c, s);
@@ -580,6 +625,13 @@ int wsg_fanout_encode_many(wsg_ctx* c, const uint8_t* d_payload, const uint64_t*
             return WSG_OK;
         if (any_payload && !d_payload)
             return WSG_EINVAL;
+        if (c->check) {
+            if (!in_alloc(d_keys, uint64_t(k) * 4) || !in_alloc(d_wire, at))
+                return WSG_EINVAL;
+            for (uint32_t i = 0; i < m; ++i)
+                if (len[i] && !in_alloc(d_payload + src_off[i], len[i]))
+                    return WSG_EINVAL;
+        }
         hipStream_t s = pick(c, stream);
         const int t = timing_begin(c, s);
         if (int rc = fanout_many(c, s, d_payload, src_off, len, opcode, m, d_keys, k, mask, d_wire, wire_off))

@@ -17,6 +17,11 @@
  * frames) are latched in the context and reported by wsg_sync.
  *
  * Thread-safety: one wsg_ctx per host thread.  A ctx is not thread-safe.
+ *
+ * Debug: with $WSG_CHECK=1 at wsg_create, the device entry points check
+ * before every launch that each operand range lies inside one device
+ * allocation (encode: every descriptor's payload range too, read back from
+ * the device) and return WSG_EINVAL instead of launching otherwise.
  */
 #ifndef WSG_CAPI_H
 #define WSG_CAPI_H

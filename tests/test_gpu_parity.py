@@ -762,3 +762,66 @@ def test_prepare_decode_matches_decode_batch(codec):
     got = ca.info_to_numpy(info, 64)
     for fld in INFO_FIELDS:
         assert np.array_equal(got[fld], info_r[fld]), fld
+
+
+def test_checked_launches(monkeypatch):
+    """$WSG_CHECK=1: operand ranges outside their device allocation are
+    refused on the host (WSG_EINVAL) before any kernel runs; valid calls give
+    the usual results.  The out-of-range operands are exact hipMalloc blocks
+    (torch's allocator hands out views of larger segments)."""
+    import ctypes
+
+    monkeypatch.setenv("WSG_CHECK", "1")
+    hip = ctypes.CDLL("libamdhip64.so.7")   # the runtime torch and libwsg share
+    blocks = []
+
+    def hip_alloc(nbytes):
+        p = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(nbytes)) == 0
+        blocks.append(p)
+        return p.value
+
+    c = ca.Codec(0)
+    try:
+        wire, fs, _ = wl.c2_wire(64, 5000, seed=5)
+        rc, out, info = gpu_decode(c, wire, fs)
+        rc_o, out_o, _ = oracle.decode_batch(wire, fs)
+        assert rc == rc_o == 0 and np.array_equal(out, out_o)
+        L = c._L
+        w = hip_alloc(2 << 20)
+        o = hip_alloc(4 << 20)
+        f = hip_alloc(64)
+        inf = hip_alloc(64)
+        vp = ctypes.c_void_p
+        assert hip.hipMemset(vp(f), 0, ctypes.c_size_t(64)) == 0
+        # decode: an output 1 MiB before the end of its 4 MiB block, 2 MiB wire
+        assert L.wsg_decode_batch(c._ctx, vp(w), 2 << 20, vp(f), 1, vp(o + (3 << 20)), vp(inf), None) == ca.WSG_EINVAL
+        # the same wire into the block's start is accepted
+        assert L.wsg_decode_batch(c._ctx, vp(w), 2 << 20, vp(f), 1, vp(o), vp(inf), None) == 0
+        # a wire length past the wire's block
+        assert L.wsg_decode_batch(c._ctx, vp(w), 3 << 20, vp(f), 1, vp(o), vp(inf), None) == ca.WSG_EINVAL
+        c.sync_status()
+        # encode: a descriptor whose payload range runs past the payload block
+        payload = hip_alloc(1 << 20)
+        desc = np.zeros(2, dtype=SEND_DESC)
+        desc["len"], desc["opcode"] = 1000, 0x82
+        desc["src_off"][1] = (1 << 20) - 10
+        d = ca.desc_to_tensor(desc, "cuda")
+        wire_o = torch.empty(4096, dtype=torch.uint8, device="cuda")
+        off = torch.empty(3, dtype=torch.int64, device="cuda")
+        args = (c._ctx, vp(payload), vp(d.data_ptr()), 2, vp(wire_o.data_ptr()), 4096, vp(off.data_ptr()), None)
+        assert L.wsg_encode_batch(*args) == ca.WSG_EINVAL
+        desc["src_off"][1] = 0
+        d.copy_(ca.desc_to_tensor(desc, "cuda"))
+        assert L.wsg_encode_batch(*args) == 0
+        assert c.sync_status() == 0 and int(off[2].item()) == 2 * 1004
+        # fan-out: 100 frames of 1004 B into a 64 KiB block with a larger stated capacity
+        keys = dev(np.arange(100, dtype=np.int32))
+        small = hip_alloc(64 << 10)
+        assert L.wsg_fanout_encode(c._ctx, vp(payload), 1000, vp(keys.data_ptr()), 100, 0x82, 1, vp(small),
+                                   1 << 20, None) == ca.WSG_EINVAL
+        torch.cuda.synchronize()
+    finally:
+        c.close()
+        for p in blocks:
+            hip.hipFree(p)
