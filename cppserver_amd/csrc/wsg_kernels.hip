@@ -102,6 +102,9 @@ __device__ __forceinline__ void st16nt(uint8_t* p, v4u v)
 #ifndef WSG_OUT_SC1
 #define WSG_OUT_SC1 0
 #endif
+#ifndef WSG_OUT_AUX
+#define WSG_OUT_AUX 16   // cache-policy bits of the write-through stores (16 = sc1, 17 = sc0 | sc1; A/B)
+#endif
 #ifndef WSG_ENC_SC1
 #define WSG_ENC_SC1 0   // batch encode (piece kernel): write-through stores (A/B)
 #endif
@@ -122,7 +125,7 @@ struct OutTile {
     __device__ __forceinline__ void put(uint32_t o, v4u v) const
     {
         if (sc1)
-            __builtin_amdgcn_raw_buffer_store_b128(v, rs, o, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, o, 0, WSG_OUT_AUX);
         else
             st16nt(p + o, v);
     }
