@@ -37,6 +37,7 @@
 #include "server/ws/wss_session.h"
 
 #include "../tests/cpp/tls_test_certs.h"
+#include "driver_options.h"
 
 #include <functional>
 
@@ -174,12 +175,27 @@ bool read_all(Pipe& p, std::vector<uint8_t>& buf, F fn)
 
 int main(int argc, char** argv)
 {
-    if (argc < 7) {
-        std::fprintf(stderr, "usage: %s per_read|tick|per_call CLIENTS THREADS MESSAGES SIZE SECONDS [tls]\n", argv[0]);
+    // positional (bench.py) or the reference's flags (ws_echo_client -c -t -m -s -z)
+    DriverOptions o;
+    o.mode = "per_read";
+    if (argc >= 7 && argv[1][0] != '-') {
+        o.mode = argv[1];
+        o.clients = std::atoi(argv[2]);
+        o.threads = std::max(1, std::atoi(argv[3]));
+        o.messages = std::atol(argv[4]);
+        o.size = std::atol(argv[5]);
+        o.seconds = std::atof(argv[6]);
+        o.tls = argc > 7 && std::string(argv[7]) == "tls";
+    } else if (!parse_driver_options(argc, argv, o)) {
+        std::fprintf(stderr,
+                     "usage: %s per_read|tick|per_call CLIENTS THREADS MESSAGES SIZE SECONDS [tls]\n"
+                     "   or: %s [--mode per_read|tick|per_call] [-c clients] [-t threads] [-m messages] [-s size] "
+                     "[-z seconds] [--tls]\n",
+                     argv[0], argv[0]);
         return 2;
     }
-    const std::string mode = argv[1];
-    const bool tls = argc > 7 && std::string(argv[7]) == "tls";
+    const std::string mode = o.mode;
+    const bool tls = o.tls;
     std::shared_ptr<CppServer::Asio::SSLContext> cctx, sctx;
     if (tls) {
         using CppServer::Asio::SSLContext;
@@ -191,9 +207,9 @@ int main(int argc, char** argv)
         cctx->set_verify_mode(CppServer::Asio::verify_peer | CppServer::Asio::verify_fail_if_no_peer_cert);
         cctx->add_certificate_authority(pki.ca_pem.data(), pki.ca_pem.size());
     }
-    const int clients = std::atoi(argv[2]), threads = std::max(1, std::atoi(argv[3]));
-    const size_t messages = std::strtoull(argv[4], nullptr, 10), size = std::strtoull(argv[5], nullptr, 10);
-    const double secs = std::atof(argv[6]);
+    const int clients = o.clients, threads = std::max(1, o.threads);
+    const size_t messages = size_t(o.messages), size = size_t(o.size);
+    const double secs = o.seconds;
     g_message.assign(size, 0);   // ws_echo_client sends zero bytes
 
     std::vector<std::unique_ptr<Conn>> conns(size_t(std::max(clients, 1)));

@@ -19,6 +19,7 @@
 //
 //   bench_multicast MODE CLIENTS RATE SIZE SECONDS
 #include "server/ws/ws_batch.h"
+#include "driver_options.h"
 #include "server/ws/ws_client.h"
 #include "server/ws/ws_handshake.h"
 #include "server/ws/ws_server.h"
@@ -98,15 +99,29 @@ void drain(Pipe& p, std::vector<uint8_t>& buf, WSSession& s)
 
 int main(int argc, char** argv)
 {
-    if (argc < 6) {
-        std::fprintf(stderr, "usage: %s per_call|tick CLIENTS RATE SIZE SECONDS\n", argv[0]);
+    // positional (bench.py) or the reference's flags (ws_multicast_server -m
+    // rate -s size, ws_multicast_client -c clients -z seconds)
+    DriverOptions o;
+    o.mode = "per_call";
+    o.messages = 1000000;   // ws_multicast_server's default rate
+    if (argc >= 6 && argv[1][0] != '-') {
+        o.mode = argv[1];
+        o.clients = std::atoi(argv[2]);
+        o.messages = std::atol(argv[3]);
+        o.size = std::atol(argv[4]);
+        o.seconds = std::atof(argv[5]);
+    } else if (!parse_driver_options(argc, argv, o)) {
+        std::fprintf(stderr,
+                     "usage: %s per_call|tick CLIENTS RATE SIZE SECONDS\n"
+                     "   or: %s [--mode per_call|tick] [-c clients] [-m rate] [-s size] [-z seconds]\n",
+                     argv[0], argv[0]);
         return 2;
     }
-    const std::string mode = argv[1];
-    const int clients = std::max(1, std::atoi(argv[2]));
-    const int rate = std::max(1, std::atoi(argv[3]));
-    const size_t size = std::strtoull(argv[4], nullptr, 10);
-    const double secs = std::atof(argv[5]);
+    const std::string mode = o.mode;
+    const int clients = std::max(1, o.clients);
+    const int rate = int(std::max(1L, o.messages));
+    const size_t size = size_t(o.size);
+    const double secs = o.seconds;
     const std::vector<uint8_t> message(size, 0);   // ws_multicast_server sends a zero-filled message
     try {
         WSServer server;
