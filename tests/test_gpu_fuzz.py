@@ -6,7 +6,9 @@ unknown), mask flags, close statuses and misaligned sources.  Every batch
 goes through the device encode (piece or small-frame kernel, whichever the
 batch selects) and decode, out of place and in place, and through the
 host-staged pair; bytes, offsets, per-frame fields and status must equal the
-oracle's.  Bit-exact, no tolerance."""
+oracle's.  Bit-exact, no tolerance.  $WSG_FUZZ_SEEDS widens the run."""
+import os
+
 import numpy as np
 import pytest
 
@@ -49,7 +51,7 @@ def _batch(seed):
     return payload, desc
 
 
-@pytest.mark.parametrize("seed", range(150))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("WSG_FUZZ_SEEDS", 150))))
 def test_fuzz_encode_decode_vs_oracle(codec, seed):
     payload, desc = _batch(1000 + seed)
     wire_o, off_o = oracle.encode_batch(payload, desc)
