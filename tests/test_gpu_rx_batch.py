@@ -3,6 +3,8 @@ oracle's per-call PrepareReceiveFrame: every session's streams are fed in the
 same interleaved order, and the batch must fire the same callbacks (kind,
 payload bytes, status) in the same global order, only later — at each flush.
 Splits inside headers included.  Bit-exact; unmask on the GPU."""
+import os
+
 import numpy as np
 import pytest
 
@@ -90,6 +92,21 @@ def test_rx_batch_over_devices_vs_oracle(codec, seed, chunk, monkeypatch):
     streams = [_stream(rng, 40, 20000) for _ in range(16)]
     expect, got = _run(codec, rng, streams, chunk, 0.05, devices=[0, 0, 0])
     assert len(expect) > 0
+    assert got == expect
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("WSG_FUZZ_SEEDS", 10))))
+def test_rx_batch_fuzz_vs_oracle(codec, seed):
+    """Random session counts, frame mixes, read sizes (down to 1 byte, so
+    headers split anywhere: SURVEY Q7) and flush points; $WSG_FUZZ_SEEDS
+    widens the run."""
+    rng = np.random.default_rng(5000 + seed)
+    chunk = [None, 2, 9, 200, 3000][int(rng.integers(0, 5))]
+    # every read is one Python call: the smaller the reads, the smaller the frames
+    sizes = {None: [10, 300, 5000, 70000], 3000: [10, 300, 5000, 70000], 200: [10, 300, 5000]}.get(chunk, [10, 300])
+    streams = [_stream(rng, int(rng.integers(1, 30)), int(rng.choice(sizes)))
+               for _ in range(int(rng.integers(1, 24)))]
+    expect, got = _run(codec, rng, streams, chunk, float(rng.choice([0.0, 0.01, 0.2])))
     assert got == expect
 
 
