@@ -129,6 +129,40 @@ def test_tx_batch_vs_oracle(codec, devices, monkeypatch):
     assert tx.pending() == (0, 0) and tx.flush() == []
 
 
+@pytest.mark.parametrize("seed", range(int(os.environ.get("WSG_FUZZ_SEEDS", 50))))
+def test_tx_batch_fuzz_vs_oracle(codec, seed):
+    """Random session counts, frame mixes and flush points (several flushes
+    per run), key changes between frames: every flush hands back its frames
+    in queue order, each the per-call encode's bytes.  $WSG_FUZZ_SEEDS
+    widens the run."""
+    rng = np.random.default_rng(9000 + seed)
+    S = int(rng.integers(1, 40))
+    sessions = [ca.Session(codec, int(rng.integers(0, 2**32))) for _ in range(S)]
+    refs = [oracle.Session() for _ in range(S)]
+    index = {id(s): i for i, s in enumerate(sessions)}
+    tx = ca.TxBatch(codec)
+    big = float(rng.choice([0.0, 0.02, 0.2]))
+    expect = []
+    for _ in range(int(rng.integers(1, 600))):
+        i = int(rng.integers(0, S))
+        op = int(rng.choice(OPCODES))
+        mask = bool(rng.random() < 0.7)
+        status = int(rng.integers(-3, 70000)) if rng.random() < 0.3 else 0
+        size = int(rng.integers(65536, 200000)) if rng.random() < big else int(rng.integers(0, 3000))
+        p = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+        if rng.random() < 0.05:
+            sessions[i].set_send_key(int(rng.integers(0, 2**32)))
+        refs[i].set_send_key(_key_of(sessions[i]))
+        expect.append((i, refs[i].prepare_send(op, mask, p, status)))
+        tx.queue(sessions[i], op, mask, p, status)
+        if rng.random() < 0.03:
+            got = tx.flush()
+            assert [(index[id(s)], f) for s, f in got] == expect
+            expect = []
+    got = tx.flush()
+    assert [(index[id(s)], f) for s, f in got] == expect
+
+
 def _key_of(session):
     """The session's current send key, read back through one encoded frame."""
     f = session.prepare_send(0x82, True, b"")
