@@ -74,3 +74,30 @@ def test_fuzz_encode_decode_vs_oracle(codec, seed):
     assert rc_h == rc_o and np.array_equal(out_h, out_o)
     for f in INFO_FIELDS:
         assert np.array_equal(info_h[f], info_o[f]), f
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("WSG_FUZZ_SEEDS", 60))))
+def test_fuzz_fanout_vs_oracle(codec, seed):
+    """Fan-out (wsg_fanout_encode): random payload length (every length class,
+    frame sizes on and off the period path), key count, opcode, mask flag and
+    source alignment; every frame vs the oracle, nothing written past the
+    last frame."""
+    rng = np.random.default_rng(7000 + seed)
+    length = int(rng.choice([int(rng.integers(0, 126)), int(rng.integers(126, 9000)),
+                             int(rng.integers(60000, 70000))]))
+    k = int(rng.integers(1, 3000 if length < 9000 else 60))
+    opcode = int(rng.choice(OPCODES))
+    mask = bool(rng.random() < 0.8)
+    src_off = int(rng.integers(0, 16))
+    payload, keys = wl.c4_fanout(length, k, seed=seed)
+    ref = oracle.fanout_encode(payload, keys, opcode, mask)
+    buf = np.zeros(length + src_off + 1, np.uint8)
+    buf[src_off: src_off + length] = payload
+    wire = torch.full((len(ref) + 48,), 0xA5, dtype=torch.uint8, device="cuda")
+    codec.fanout(torch.from_numpy(buf).cuda()[src_off:], torch.from_numpy(keys.view(np.int32)).cuda(), opcode, mask,
+                 wire=wire, length=length)
+    codec.sync()
+    got = wire.cpu().numpy()
+    bad = np.nonzero(got[: len(ref)] != ref)[0]
+    assert bad.size == 0, "first mismatch at byte %d of %d" % (bad[0], len(ref))
+    assert (got[len(ref):] == 0xA5).all()
