@@ -245,6 +245,26 @@ class Codec:
 
         return launch
 
+    def prepare_fanout(self, payload, keys, opcode, mask, wire, length=None, stream=None):
+        """wsg_fanout_encode on fixed buffers with the ctypes arguments bound
+        once (the multicast loop of a server); returns a launch callable."""
+        k = int(keys.numel())
+        length = int(payload.numel()) if length is None else int(length)
+        assert frame_size(opcode, mask, length) * k <= int(wire.numel())
+        fn = self._L.wsg_fanout_encode
+        args = (self._ctx, ctypes.c_void_p(payload.data_ptr()), ctypes.c_uint64(length),
+                ctypes.c_void_p(keys.data_ptr()), ctypes.c_uint32(k), ctypes.c_uint8(opcode), 1 if mask else 0,
+                ctypes.c_void_p(wire.data_ptr()), ctypes.c_uint64(wire.numel()), self._stream(stream))
+        keep = (payload, keys, wire)
+
+        def launch():
+            rc = fn(*args)
+            if rc != 0:
+                raise WSGError(rc, "wsg_fanout_encode")
+            return keep
+
+        return launch
+
     # -- batch encode (mask) --------------------------------------------------
     def encode_batch(self, payload, desc, wire=None, wire_cap=None, wire_off=None, stream=None):
         """Encode frames ``desc`` (uint8 CUDA tensor of n*32 bytes) whose data

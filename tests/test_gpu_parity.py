@@ -825,3 +825,17 @@ def test_checked_launches(monkeypatch):
         c.close()
         for p in blocks:
             hip.hipFree(p)
+
+
+def test_prepare_fanout_matches_oracle(codec):
+    """Codec.prepare_fanout (the bench's pre-bound C-ABI fan-out) writes the
+    oracle's frames, launch after launch."""
+    payload, keys = wl.c4_fanout(4096, 777, seed=31)
+    ref = oracle.fanout_encode(payload, keys, 0x82, True)
+    wire = torch.full((len(ref) + 32,), 0xA5, dtype=torch.uint8, device="cuda")
+    launch = codec.prepare_fanout(dev(payload), dev(keys.view(np.int32)), 0x82, True, wire)
+    for _ in range(3):
+        launch()
+    assert codec.sync_status() == 0
+    got = wire.cpu().numpy()
+    assert np.array_equal(got[: len(ref)], ref) and (got[len(ref):] == 0xA5).all()
