@@ -11,8 +11,12 @@ process per GPU; every rank decodes its own independent batch of the same
 shape (frames shard with no data-path collective: weak scaling); the timed
 region is bracketed by barrier + synchronize and the max over ranks is used.
 
-Other configs (--config c3|c4|c5) are available for tracking; the headline
-line is c2.
+The default N=1 run also measures the other BASELINE configs, each as a
+bounded leg with its own object in the line ("c3", "c4", "c5": value,
+ms_per_step, roofline of its dominant kernels -- C3 both halves of the round
+trip --, CPU baseline, spot check): C3 mask+unmask round trip of 65536 ragged
+frames, C4 fan-out of one 4 KiB payload to 10000 keys, C5 the whole 1 Mi x
+16 KiB job on this GPU.  --config c3|c4|c5 makes one of them the headline.
 """
 import argparse
 import json
@@ -44,6 +48,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip copy-ceiling and PCIe-inclusive legs")
+    ap.add_argument("--no-configs", action="store_true", help="c2 at N=1: skip the C3/C4/C5 legs")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -191,6 +196,11 @@ class Workload:
             self.payload_bytes = int(desc["len"].sum())
             self.alg_bytes = len(payload) + cap        # encode mask kernel: read payload + write wire
             self.kernel = "k_encode_mask"
+            # the round trip's second half, k_decode: read wire + write out,
+            # plus per frame its start (8 B) and wsg_recv_info (32 B); timed on
+            # a context of its own so each half has its own HIP events
+            self.dec_alg_bytes = 2 * cap + n * 40
+            self.dec_codec = ca.Codec(device.index if device.index is not None else 0)
             self.workload = "C3 mask+unmask round trip: %d frames, payload uniform in [128, 65536] B" % n
             self.extra = {"frames": n, "wire_bytes": cap}
         elif self.cfg == "c4":
@@ -248,6 +258,15 @@ class Workload:
             self.workload = "C5 encode shard: %d x %d B frames of a %d-frame job (round-robin)" % (n, size, n_total)
             self.extra = {"frames_this_rank": n, "wire_bytes": cap}
 
+    def close(self):
+        """Free the device buffers (and C3's decode context) before the next leg."""
+        if getattr(self, "dec_codec", None) is not None:
+            self.dec_codec.close()
+            self.dec_codec = None
+        for name in ("wire", "fs", "out", "batches", "launch", "info", "payload", "desc", "woff", "keys"):
+            if hasattr(self, name):
+                setattr(self, name, None)
+
     def step(self):
         c = self.codec
         if self.cfg == "c2":
@@ -255,7 +274,7 @@ class Workload:
             self.turn ^= 1
         elif self.cfg == "c3":
             c.encode_batch(self.payload, self.desc, wire=self.wire, wire_cap=self.cap, wire_off=self.woff)
-            c.decode_batch(self.wire, self.woff[:-1], out=self.out, info=self.info)
+            self.dec_codec.decode_batch(self.wire, self.woff[:-1], out=self.out, info=self.info)
         elif self.cfg == "c4":
             if self.m == 1:
                 self.launch()
@@ -536,9 +555,27 @@ def echo_c1_leg(seconds=3.0, timeout=120):
             continue
         d = json.loads(r.stdout.strip().splitlines()[-1])
         out[leg] = {k: d[k] for k in ("msg_per_s", "MiB_per_s", "latency_ns", "total_messages", "payload_ok")}
+    # the reference's algorithm in the SAME loop: the oracle's restatement of
+    # PrepareSendFrame / PrepareReceiveFrame (CPU, no GPU) driving the same
+    # in-memory echo (tools/_build/bench_echo_ref; the cpu_baseline side)
+    ref = os.path.join(ROOT, "tools", "_build", "bench_echo_ref")
+    if os.path.exists(ref):
+        cr = {}
+        for leg, a in (("1c_1t", ["1", "1", "1000", "32"]), ("100c_4t", ["100", "4", "1000", "32"])):
+            r = subprocess.run([ref] + a + [str(seconds)], capture_output=True, text=True, timeout=timeout)
+            if r.returncode != 0:
+                cr[leg] = {"error": (r.stderr or r.stdout).strip()[-300:]}
+                continue
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            cr[leg] = {k: d[k] for k in ("msg_per_s", "MiB_per_s", "latency_ns", "total_messages", "payload_ok")}
+        cr["what"] = ("reference codec algorithm (oracle restatement of ws.cpp:212-456, CPU) in this same in-memory "
+                      "echo loop; compare with per_read_1c / per_read_100c_4t")
+        out["cpu_reference"] = cr
     out["reference_published"] = {"msg_per_s_1c_1t": 160448, "msg_per_s_100c_4t": 594328,
                                   "wss_msg_per_s_1c_1t": 203343, "wss_msg_per_s_100c_4t": 818230,
-                                  "hardware": "i7-4790K, loopback sockets (README.md:3312-3352, 3356-3396)"}
+                                  "hardware": "loopback sockets, i7-4790K (README.md:3312-3352, 3356-3396): "
+                                              "not like-for-like with this in-memory loop"}
+    out["transport"] = "in-memory pipes, no socket syscalls (sockets are out of scope)"
     return out
 
 
@@ -567,7 +604,10 @@ def multicast_leg(seconds=2.0, timeout=120):
         d = json.loads(r.stdout.strip().splitlines()[-1])
         out[leg] = {k: d[k] for k in ("msg_per_s", "MiB_per_s", "total_messages", "all_delivered")}
     out["reference_published"] = {"msg_per_s_1c_1t": 3148135, "msg_per_s_100c_4t": 3225965,
-                                  "hardware": "i7-4790K, loopback sockets (README.md:3542-3580)"}
+                                  "hardware": "loopback sockets, i7-4790K (README.md:3542-3580): not like-for-like "
+                                              "with this in-memory loop"}
+    out["gpu_work"] = ("none: server frames carry key 0 (ws.cpp:206), the XOR is the identity; this measures the "
+                       "API's framing and fan-out copies (the keyed GPU fan-out is C4)")
     return out
 
 
@@ -860,6 +900,152 @@ def fanout_many_leg(w, m=16, reps=10):
             "write_GBps": round(bytes_out / (ms * 1e-3) / 1e9, 1), "frame_bytes": fsz}
 
 
+def roofline_obj(kernel, alg_bytes, avg_ms, traffic, timing):
+    """The roofline object of one kernel: algorithmic bytes per launch over
+    its average launch duration (HIP events on its launch stream), against
+    the HBM peak; `traffic` = PMC HBM bytes per launch (profiles/), or None."""
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms else 0.0
+    return {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
+            "avg_kernel_ms": round(avg_ms, 5), "kernel_timing": timing}
+
+
+def timed_region(w, steps, world, device):
+    """EXACTLY `steps` steps between barrier + torch.cuda.synchronize() on
+    both sides (wall clock, max over ranks), with the dominant kernels' HIP
+    events.  C2/C4 steps are ONE launch of the dominant kernel, so two events
+    around the region on its launch stream (torch's current stream) give its
+    average duration without adding anything between launches; C3/C5 steps
+    launch several kernels, so the library times the dominant one of every
+    `every`-th call (each event pair costs a few us: every 8th call for long
+    regions, every call for the short sub-config regions)."""
+    import torch
+
+    single = w.cfg in ("c2", "c4")
+    codecs = [w.codec] + ([w.dec_codec] if w.cfg == "c3" else [])
+    every = 1 if steps <= 20 else 8
+    if not single:
+        for c in codecs:
+            c.timing(True, every=every)
+            c.timing_read(reset=True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # torch creates the HIP events at their first record(): do that here, not
+    # inside the timed region (a first hipEventCreate costs tens of us)
+    e0.record()
+    e1.record()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(steps):
+        w.step()
+    e1.record()
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    region_ms = e0.elapsed_time(e1)
+    if single:
+        kern = [(region_ms, steps)]
+        note = "HIP events around the timed region / steps (one launch per step)"
+    else:
+        kern = []
+        for c in codecs:
+            kern.append(c.timing_read(reset=True))
+            c.timing(False)
+        note = ("HIP events around the dominant kernel of every call in the timed region" if every == 1 else
+                "HIP events around the dominant kernel of every %dth call in the timed region" % every)
+    w.codec.sync()
+    elapsed = max_over_ranks(elapsed, world, device)
+    avgs = [max_over_ranks(ms / max(k, 1), world, device) for ms, k in kern]
+    return {"elapsed": elapsed, "region_event_ms": region_ms, "kernel_avg_ms": avgs, "timing": note}
+
+
+def config_obj(args, cfg, codec, rank, world, device, steps, warmup, cpu):
+    """One BASELINE config measured in this run: its own workload, spot check
+    against the oracle, warm-up, timed region, roofline per dominant kernel
+    (C3: both halves of the round trip), and the CPU baseline beside it."""
+    import argparse as _ap
+
+    sub = _ap.Namespace(**dict(vars(args), config=cfg, frames=None, size=None, messages=1))
+    w = Workload(sub, codec, rank, device)
+    try:
+        ok = w.spot_check()
+        # warm-up by time: after the seconds of host work above (input
+        # generation, the oracle spot check) the GPU has sat idle, and the
+        # first ~15 ms of load run up to 25 % slower (tools/c3_dec.py:
+        # C3's decode 0.88 -> 0.69 ms over its first 20 launches)
+        warmup = warm_up(w, warmup, WARM_SECONDS)
+        r = timed_region(w, steps, world, device)
+        ms_step = r["elapsed"] / steps * 1e3
+        obj = {"workload": w.workload, "value": round(world * w.payload_bytes * steps / r["elapsed"] / GIB, 2),
+               "unit": "GiB/s", "steps": steps, "warmup": warmup, "ms_per_step": round(ms_step, 4),
+               "event_ms_per_step": round(r["region_event_ms"] / steps, 4)}
+        obj.update(w.extra)
+        rf = roofline_obj(w.kernel, w.alg_bytes, r["kernel_avg_ms"][0], pmc_traffic(args.pmc, cfg), r["timing"])
+        if cfg == "c3":
+            dec = roofline_obj("k_decode", w.dec_alg_bytes, r["kernel_avg_ms"][1], pmc_traffic(args.pmc, "c3_dec"),
+                               r["timing"])
+            both = w.alg_bytes + w.dec_alg_bytes
+            t = sum(r["kernel_avg_ms"])
+            rf = dict(dec, halves=[rf, dec],
+                      round_trip={"alg_bytes": both, "kernel_ms": round(t, 5),
+                                  "achieved": round(both / (t * 1e-3) / 1e9, 1),
+                                  "frac": round(both / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)})
+        obj["roofline"] = rf
+        if cfg == "c3":
+            obj["k_decode_per_launch"] = decode_launches(w)
+        if cpu is not None and rank == 0:
+            c1, cn = cpu_baseline(w, args.cpu_seconds * 0.6, cpu)
+            obj["cpu_baseline"], obj["cpu_baseline_mt"] = c1, cn
+        obj["spot_check"] = ok
+        return obj
+    finally:
+        w.close()
+
+
+def decode_launches(w, launches=30):
+    """C3's decode half launch by launch: k_decode alone
+    on the round trip's wire, HIP events between launches (one launch per
+    decode_batch call), after the timed region (the GPU is warm)."""
+    import statistics
+
+    t = w.torch
+    ev = [t.cuda.Event(enable_timing=True) for _ in range(launches + 1)]
+    for e in ev:
+        e.record()
+    t.cuda.synchronize()
+    ev[0].record()
+    for i in range(launches):
+        w.dec_codec.decode_batch(w.wire, w.woff[:-1], out=w.out, info=w.info)
+        ev[i + 1].record()
+    t.cuda.synchronize()
+    ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(launches)]
+    med = statistics.median(ms)
+    return {"launches": launches, "median_ms": round(med, 5), "min_ms": round(min(ms), 5),
+            "max_ms": round(max(ms), 5), "spread_pct": round(100 * (max(ms) - min(ms)) / med, 2),
+            "frac_at_median": round(w.dec_alg_bytes / (med * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+
+
+SUB_CONFIGS = (("c3", 20, 3), ("c4", 200, 3), ("c5", 10, 3))   # (config, steps, min warm-up steps): bounded legs
+WARM_SECONDS = 0.25
+
+
+def warm_up(w, min_steps, seconds):
+    """Untimed steps: at least `min_steps`, and until `seconds` of them have
+    run on the GPU.  Returns the number of steps."""
+    import torch
+
+    done = 0
+    t0 = time.perf_counter()
+    while done < min_steps or time.perf_counter() - t0 < seconds:
+        for _ in range(max(1, min_steps)):
+            w.step()
+        done += max(1, min_steps)
+        torch.cuda.synchronize()
+    w.codec.sync()
+    return done
+
+
 def main():
     args = parse()
     import torch
@@ -880,45 +1066,20 @@ def main():
         w.step()
     codec.sync()
 
-    # Kernel time, live over the timed region, on the stream the kernels are
-    # launched on (torch's current stream).  C2 and C4 steps are ONE launch
-    # of the dominant kernel, so two events around the region give its
-    # average duration (launch gaps included: an upper bound) without adding
-    # anything between launches.  C3/C5 steps launch several kernels: HIP
-    # events around the dominant one of every 8th step (each event packet
-    # costs a few us, so timing every step would slow the step itself).
-    single = w.cfg in ("c2", "c4")
-    if not single:
-        codec.timing(True, every=8)
-        codec.timing_read(reset=True)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e0.record()
-    for _ in range(args.steps):
-        w.step()
-    e1.record()
-    torch.cuda.synchronize()
-    barrier(world)
-    elapsed = time.perf_counter() - t0
-    if single:
-        kernel_ms, launches = e0.elapsed_time(e1), args.steps
-    else:
-        kernel_ms, launches = codec.timing_read(reset=True)
-        codec.timing(False)
-    codec.sync()
-
-    elapsed = max_over_ranks(elapsed, world, device)
+    r = timed_region(w, args.steps, world, device)
+    elapsed = r["elapsed"]
     ms_per_step = elapsed / args.steps * 1e3
     value = world * w.payload_bytes * args.steps / elapsed / GIB
-    k_avg_ms = kernel_ms / max(launches, 1)
-    k_avg_ms = max_over_ranks(k_avg_ms, world, device)
-    achieved = w.alg_bytes / (k_avg_ms * 1e-3) / 1e9
+    k_avg_ms = r["kernel_avg_ms"][0]
     pmc_key = w.cfg + ("x%d" % w.m if w.cfg == "c4" and w.m > 1 else "")
     traffic = pmc_traffic(args.pmc, pmc_key) if args.frames is None and args.size is None else None
+    roof = roofline_obj(w.kernel, w.alg_bytes, k_avg_ms, traffic, r["timing"])
+    if w.cfg == "c3":
+        dec = roofline_obj("k_decode", w.dec_alg_bytes, r["kernel_avg_ms"][1],
+                           pmc_traffic(args.pmc, "c3_dec") if traffic is not None else None, r["timing"])
+        roof = dict(dec, halves=[roof, dec])
 
-    extras = {}
+    extras = {"event_ms_per_step": round(r["region_event_ms"] / args.steps, 4)}
     if w.cfg == "c5" and world > 1:
         extras["gather"] = gather_leg(w, world, rank, device)
     if w.cfg == "c2" and world > 1 and not args.no_extras:
@@ -938,6 +1099,10 @@ def main():
             capi = c5_capi_leg(world, rank, n_total=int(os.environ.get("WSG_C5_FRAMES", 1 << 20)))
             if capi is not None:
                 extras["c5_job_capi"] = capi
+    cpu = host_cpu() if (rank == 0 and world == 1 and not args.no_cpu) else None
+    cpu1 = cpu_mt = None
+    if cpu is not None:
+        cpu1, cpu_mt = cpu_baseline(w, args.cpu_seconds, cpu)
     if rank == 0 and world == 1 and not args.no_extras:
         extras["copy_ceiling_GBps"] = round(copy_ceiling(w), 1)
         pc = pcie_inclusive(w)
@@ -948,18 +1113,31 @@ def main():
             extras["fanout_many"] = fanout_many_leg(w)
         if w.cfg == "c2":
             extras["echo_size_device"] = echo_size_leg(w)
-            sb = session_batch_leg()
-            if sb is not None:
-                extras["session_batch"] = sb
-            c1 = echo_c1_leg()
-            if c1 is not None:
-                extras["echo_c1"] = c1
-            mc = multicast_leg()
-            if mc is not None:
-                extras["ws_multicast"] = mc
-    cpu1 = cpu_mt = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu1, cpu_mt = cpu_baseline(w, args.cpu_seconds, host_cpu())
+    headline_cfg = w.cfg
+    workload_name, workload_extra = w.workload, w.extra
+    w.close()
+    del w
+    torch.cuda.empty_cache()
+    # the other BASELINE configs (C3 round trip, C4 fan-out, C5 1 Mi x 16 KiB
+    # job on this GPU), each a bounded leg with its own roofline and CPU
+    # baseline, after the headline's own region (its inputs are freed first)
+    if headline_cfg == "c2" and world == 1 and not args.no_configs:
+        for cfg, steps, warm in SUB_CONFIGS:
+            try:
+                extras[cfg] = config_obj(args, cfg, codec, rank, world, device, steps, warm, cpu)
+            except Exception as e:   # noqa: BLE001  (reported; the headline stands)
+                extras[cfg] = {"error": repr(e)[:300]}
+            torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_extras and headline_cfg == "c2":
+        sb = session_batch_leg()
+        if sb is not None:
+            extras["session_batch"] = sb
+        c1 = echo_c1_leg()
+        if c1 is not None:
+            extras["echo_c1"] = c1
+        mc = multicast_leg()
+        if mc is not None:
+            extras["ws_multicast"] = mc
 
     if world > 1:
         import torch.distributed as dist
@@ -969,8 +1147,9 @@ def main():
         ok = bool(okt.item())
 
     if rank == 0:
+        cfg = args.config
         line = {
-            "metric": METRIC if w.cfg == "c2" else "WS payload GiB/s (device-resident), " + w.cfg.upper(),
+            "metric": METRIC if cfg == "c2" else "WS payload GiB/s (device-resident), " + cfg.upper(),
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -978,26 +1157,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "strong" if w.cfg == "c5" else "weak",
+            "scaling": "strong" if cfg == "c5" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded random payloads and keys)",
-            "config": dict({"workload": w.workload,
-                            "parallelism": ("1 Mi-frame job split round-robin over %d GPUs" % world) if w.cfg == "c5"
-                            else "independent batch per GPU (dp%d)" % world}, **w.extra),
-            "roofline": {
-                "bound": "hbm",
-                "kernel": w.kernel,
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic,
-                "alg_bytes_per_launch": w.alg_bytes,
-                "avg_kernel_ms": round(k_avg_ms, 5),
-                "kernel_timing": ("HIP events around the timed region / steps (one launch per step)" if single
-                                  else "HIP events around every 8th launch in the timed region"),
-            },
+            "config": dict({"workload": workload_name,
+                            "parallelism": ("1 Mi-frame job split round-robin over %d GPUs" % world) if cfg == "c5"
+                            else "independent batch per GPU (dp%d)" % world}, **workload_extra),
+            "roofline": roof,
             "cpu_baseline": cpu1,
             "cpu_baseline_mt": cpu_mt,
             "spot_check": ok,

@@ -230,15 +230,18 @@ class Codec:
         the ctypes arguments bound once: returns a callable that launches one
         decode per call (asynchronous, like decode_batch)."""
         n = int(frame_start.numel())
-        assert int(out.numel()) >= int(wire.numel()) and int(info.numel()) >= n * RECV_INFO.itemsize
-        fn, st = self._L.wsg_decode_batch, self._stream(stream)
+        if int(out.numel()) < int(wire.numel()) or int(info.numel()) < n * RECV_INFO.itemsize:
+            raise WSGError(WSG_EINVAL, "prepare_decode: out or info smaller than the batch needs")
+        fn = self._L.wsg_decode_batch
         args = (self._ctx, ctypes.c_void_p(wire.data_ptr()), ctypes.c_uint64(wire.numel()),
                 ctypes.c_void_p(frame_start.data_ptr()), ctypes.c_uint32(n), ctypes.c_void_p(out.data_ptr()),
-                ctypes.c_void_p(info.data_ptr()), st)
+                ctypes.c_void_p(info.data_ptr()))
         keep = (wire, frame_start, out, info)   # the buffers live as long as the callable
+        fixed = None if stream is None else self._stream(stream)
 
         def launch():
-            rc = fn(*args)
+            # stream=None: torch's current stream at each launch, as decode_batch
+            rc = fn(*args, fixed if fixed is not None else self._stream(None))
             if rc != 0:
                 raise WSGError(rc, "wsg_decode_batch")
             return keep
@@ -250,15 +253,18 @@ class Codec:
         once (the multicast loop of a server); returns a launch callable."""
         k = int(keys.numel())
         length = int(payload.numel()) if length is None else int(length)
-        assert frame_size(opcode, mask, length) * k <= int(wire.numel())
+        if frame_size(opcode, mask, length) * k > int(wire.numel()):
+            raise WSGError(WSG_ENOMEM, "prepare_fanout: wire smaller than %d frames" % k)
         fn = self._L.wsg_fanout_encode
         args = (self._ctx, ctypes.c_void_p(payload.data_ptr()), ctypes.c_uint64(length),
                 ctypes.c_void_p(keys.data_ptr()), ctypes.c_uint32(k), ctypes.c_uint8(opcode), 1 if mask else 0,
-                ctypes.c_void_p(wire.data_ptr()), ctypes.c_uint64(wire.numel()), self._stream(stream))
+                ctypes.c_void_p(wire.data_ptr()), ctypes.c_uint64(wire.numel()))
         keep = (payload, keys, wire)
+        fixed = None if stream is None else self._stream(stream)
 
         def launch():
-            rc = fn(*args)
+            # stream=None: torch's current stream at each launch, as fanout
+            rc = fn(*args, fixed if fixed is not None else self._stream(None))
             if rc != 0:
                 raise WSGError(rc, "wsg_fanout_encode")
             return keep
@@ -603,11 +609,14 @@ def encode_batch_host_multi(codecs, payload, desc, wire=None):
 
 class MultiGPU:
     """The multi-GPU entry of the C-ABI (wsg_mgpu_*): round-robin shards of a
-    frame batch encoded on their GPUs and gathered to one rank over RCCL.
+    frame batch encoded on their GPUs and gathered to one rank.
 
-    MultiGPU(devices=[0, 1, ...]) drives several GPUs from this process;
+    MultiGPU(devices=[0, 1, ...]) drives every rank from this process, one
+    rank per listed device (a device may be listed more than once): chunks
+    move to the root by device copies (xGMI peer copies between GPUs);
     MultiGPU.rank(device, uid, rank, world) is one rank of a multi-process
-    group (uid from MultiGPU.unique_id() on rank 0, handed to every rank)."""
+    group over RCCL (uid from MultiGPU.unique_id() on rank 0, handed to
+    every rank)."""
 
     ID_BYTES = 128
 

@@ -513,6 +513,16 @@ size_t TLSTransport::Receive(void* buffer, size_t size, const CppCommon::Timespa
             }
             if (_failed || !_handshaked)
                 return 0;
+            // bytes held back for a batch scope or a feed in progress go out
+            // before we wait for the reply to them (a request sent with
+            // SendAsync inside a scope, then a synchronous receive)
+            if (!_out_plain.empty()) {
+                std::vector<uint8_t> p, rec;
+                p.swap(_out_plain);
+                encrypt(p.data(), p.size(), rec);
+                if (!rec.empty())
+                    _lower.SendAsync(rec.data(), rec.size());
+            }
         }
         const size_t n = timeout.total() ? _lower.Receive(in.data(), in.size(), timeout)
                                          : _lower.Receive(in.data(), in.size());

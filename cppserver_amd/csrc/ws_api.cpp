@@ -58,9 +58,8 @@ void WSClient::ResetBuffers()
 
 WSClient::~WSClient()
 {
-    // frames still queued on this thread's automatic batches
-    BatchScope::Receive().Forget(*this);
-    BatchScope::Send().Forget(_transport);
+    // frames still queued on any thread's automatic batches
+    BatchScope::ForgetEverywhere(*this, _transport);
 }
 
 void WSClient::SetReceiveBatch(WSReceiveBatch* batch)
@@ -153,10 +152,16 @@ void WSClient::RouteFrames(const void* buffer, size_t size)
 
 void WSClient::SetSendBatch(WSSendBatch* batch)
 {
-    std::scoped_lock locker(_ws_send_lock);
-    if (_tx_batch && _tx_batch != batch)
-        _tx_batch->Forget(_transport);
-    _tx_batch = batch;
+    WSSendBatch* old;
+    {
+        std::scoped_lock locker(_ws_send_lock);
+        old = _tx_batch;
+        _tx_batch = batch;
+    }
+    // not under the send lock: Forget may wait for a flush on another thread
+    // whose deliveries take session send locks (a multicast)
+    if (old && old != batch)
+        old->Forget(_transport);
 }
 
 size_t WSClient::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status,
@@ -249,8 +254,8 @@ void WSSession::ResetBuffers()
 
 WSSession::~WSSession()
 {
-    BatchScope::Receive().Forget(*this);
-    BatchScope::Send().Forget(_transport);
+    // frames still queued on any thread's automatic batches
+    BatchScope::ForgetEverywhere(*this, _transport);
 }
 
 void WSSession::SetReceiveBatch(WSReceiveBatch* batch)
@@ -326,10 +331,16 @@ void WSSession::RouteFrames(const void* buffer, size_t size)
 
 void WSSession::SetSendBatch(WSSendBatch* batch)
 {
-    std::scoped_lock locker(_ws_send_lock);
-    if (_tx_batch && _tx_batch != batch)
-        _tx_batch->Forget(_transport);
-    _tx_batch = batch;
+    WSSendBatch* old;
+    {
+        std::scoped_lock locker(_ws_send_lock);
+        old = _tx_batch;
+        _tx_batch = batch;
+    }
+    // not under the send lock: Forget may wait for a flush on another thread
+    // whose deliveries take session send locks (a multicast)
+    if (old && old != batch)
+        old->Forget(_transport);
 }
 
 size_t WSSession::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status,

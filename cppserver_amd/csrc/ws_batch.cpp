@@ -200,12 +200,38 @@ void WSReceiveBatch::Clear(WebSocket& ws)
 
 void WSReceiveBatch::Forget(WebSocket& ws)
 {
-    std::scoped_lock locker(_lock);
-    for (Batch* b : {&_cur, &_spare})
-        for (Rec& r : b->recs)
+    std::unique_lock<std::mutex> locker(_lock);
+    for (Rec& r : _cur.recs)
+        if (r.ws == &ws)
+            r.ws = nullptr;
+    if (!_flushing)
+        return;
+    if (_flusher == std::this_thread::get_id()) {
+        // from a callback of this thread's flush: its records are this thread's
+        for (Rec& r : _spare.recs)
             if (r.ws == &ws)
                 r.ws = nullptr;
-    _forgets.fetch_add(1, std::memory_order_release);
+        return;
+    }
+    // another thread is delivering: it drops ws's frames before its next
+    // record (after the callback it may be running now), then wakes us
+    _pending.push_back(&ws);
+    _has_pending.store(true, std::memory_order_release);
+    const uint64_t at = _applied;
+    _applied_cv.wait(locker, [&] { return _applied != at; });
+}
+
+void WSReceiveBatch::ApplyPending(size_t from)
+{
+    // the flushing thread, _lock held
+    for (WebSocket* ws : _pending)
+        for (size_t r = from; r < _spare.recs.size(); ++r)
+            if (_spare.recs[r].ws == ws)
+                _spare.recs[r].ws = nullptr;
+    _pending.clear();
+    _has_pending.store(false, std::memory_order_relaxed);
+    ++_applied;
+    _applied_cv.notify_all();
 }
 
 size_t WSReceiveBatch::Flush()
@@ -217,6 +243,7 @@ size_t WSReceiveBatch::Flush()
         std::swap(_cur, _spare);
         _cur.reset();
         _flushing = true;
+        _flusher = std::this_thread::get_id();
     }
     Batch& b = _spare;   // this thread's until _flushing drops: Feed only touches _cur
     struct Done {
@@ -226,6 +253,7 @@ size_t WSReceiveBatch::Flush()
             std::scoped_lock locker(t->_lock);
             t->_flushing = false;
             t->_spare.reset();
+            t->ApplyPending(0);   // nothing left to deliver: release any waiting Forget
         }
     } done{this};
 
@@ -261,18 +289,14 @@ size_t WSReceiveBatch::Flush()
         }
     }
     size_t delivered = 0;
-    // the records as of the swap; a Forget() (a callback dropping a
-    // connection) makes the rest be re-read under the lock
-    const std::vector<Rec> snap = b.recs;
-    uint64_t seen = _forgets.load(std::memory_order_acquire);
-    bool relock = false;
-    for (size_t r = 0; r < snap.size(); ++r) {
-        Rec rec = snap[r];
-        if (relock || _forgets.load(std::memory_order_acquire) != seen) {
-            relock = true;
+    // b.recs is written only by this thread (its callbacks' Forget); other
+    // threads' Forget()s are applied here, between two records
+    for (size_t r = 0; r < b.recs.size(); ++r) {
+        if (_has_pending.load(std::memory_order_acquire)) {
             std::scoped_lock locker(_lock);
-            rec = b.recs[r];
+            ApplyPending(r);
         }
+        const Rec rec = b.recs[r];
         if (!rec.ws)
             continue;
         if (rec.frame < 0) {
@@ -369,24 +393,50 @@ void WSSendBatch::QueueFanout(std::function<void(const uint8_t*, size_t)> delive
          key, opcode, mask, buffer, size, status);
 }
 
-void WSSendBatch::Forget(Transport& transport)
+void WSSendBatch::Forget(Transport& transport) { ForgetIf(&transport, nullptr); }
+
+void WSSendBatch::Forget(void* tag) { ForgetIf(nullptr, tag); }
+
+namespace {
+bool rec_matches(Transport* rt, void* rtag, Transport* transport, void* tag)
 {
-    std::scoped_lock locker(_lock);
-    for (Queue_* q : {&_q, &_inflight})
-        for (Rec& r : q->recs)
-            if (r.transport == &transport)
+    return transport ? rt == transport : (rtag == tag && !rt);
+}
+} // namespace
+
+void WSSendBatch::ForgetIf(Transport* transport, void* tag)
+{
+    std::unique_lock<std::mutex> locker(_lock);
+    for (Rec& r : _q.recs)
+        if (rec_matches(r.transport, r.tag, transport, tag))
+            r = Rec{nullptr, nullptr, nullptr};
+    if (!_flushing)
+        return;
+    if (_flusher == std::this_thread::get_id()) {   // from a callback of this thread's flush
+        for (Rec& r : _inflight.recs)
+            if (rec_matches(r.transport, r.tag, transport, tag))
                 r = Rec{nullptr, nullptr, nullptr};
-    _forgets.fetch_add(1, std::memory_order_release);
+        return;
+    }
+    _pending.emplace_back(transport, tag);   // applied by the flush before its next frame
+    _has_pending.store(true, std::memory_order_release);
+    const uint64_t at = _applied;
+    _applied_cv.wait(locker, [&] { return _applied != at; });
 }
 
-void WSSendBatch::Forget(void* tag)
+void WSSendBatch::ApplyPending(size_t from)
 {
-    std::scoped_lock locker(_lock);
-    for (Queue_* q : {&_q, &_inflight})
-        for (Rec& r : q->recs)
-            if (r.tag == tag && !r.transport)
+    // the flushing thread, _lock held
+    for (const auto& p : _pending)
+        for (size_t i = from; i < _inflight.recs.size(); ++i) {
+            Rec& r = _inflight.recs[i];
+            if (rec_matches(r.transport, r.tag, p.first, p.second))
                 r = Rec{nullptr, nullptr, nullptr};
-    _forgets.fetch_add(1, std::memory_order_release);
+        }
+    _pending.clear();
+    _has_pending.store(false, std::memory_order_relaxed);
+    ++_applied;
+    _applied_cv.notify_all();
 }
 
 size_t WSSendBatch::Flush(Sink sink, void* user)
@@ -400,6 +450,7 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
         _q.desc.clear();
         _q.recs.clear();
         _flushing = true;
+        _flusher = std::this_thread::get_id();
     }
     struct Done {
         WSSendBatch* t;
@@ -410,6 +461,7 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
             t->_inflight.payload.len = 0;
             t->_inflight.desc.clear();
             t->_inflight.recs.clear();
+            t->ApplyPending(0);   // nothing left to hand out: release any waiting Forget
         }
     } done{this};
     Queue_& b = _inflight;
@@ -457,6 +509,7 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
         // nothing was handed out: the frames go back in front of anything
         // queued meanwhile, so a later flush still sends them in order
         std::scoped_lock locker(_lock);
+        ApplyPending(0);   // forgotten frames are not requeued
         const uint64_t shift = b.payload.len;
         grow_pinned(b.payload.p, b.payload.cap, b.payload.len, b.payload.len + _q.payload.len);
         if (_q.payload.len)
@@ -475,21 +528,16 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
         check(rc, "wsg_encode_batch_host");
     }
     size_t sent = 0;
-    // records as of the swap; after a Forget() the rest are re-read under the lock
-    const uint64_t seen = _forgets.load(std::memory_order_acquire);
-    bool relock = false;
+    // b.recs is written only by this thread (its callbacks' Forget); other
+    // threads' Forget()s are applied here, between two frames
     for (uint32_t i = 0; i < n; ++i) {
         const uint8_t* f = _wire.p + _wire_off[i];
         const size_t len = size_t(_wire_off[i + 1] - _wire_off[i]);
-        const Rec* rp = &b.recs[i];   // only this flush writes b.recs' length; Forget() writes entries
-        Rec rec;
-        if (relock || _forgets.load(std::memory_order_acquire) != seen) {
-            relock = true;
+        if (_has_pending.load(std::memory_order_acquire)) {
             std::scoped_lock locker(_lock);
-            rec = *rp;
-        } else {
-            rec = *rp;
+            ApplyPending(i);
         }
+        const Rec rec = b.recs[i];
         if (rec.transport) {
             rec.transport->SendAsync(f, len);
             ++sent;
@@ -508,14 +556,42 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
 
 namespace {
 
+// Every thread's automatic batches, so that a connection being destroyed can
+// drop what it queued into another thread's scope (ForgetEverywhere).  The
+// batches are shared: one outlives its thread while a ForgetEverywhere uses it.
+struct AutoEntry {
+    std::weak_ptr<WSReceiveBatch> rx;
+    std::weak_ptr<WSSendBatch> tx;
+};
+std::mutex& auto_registry_lock()
+{
+    static std::mutex* m = new std::mutex;   // leaked: used from thread exits after static destruction
+    return *m;
+}
+std::vector<AutoEntry>& auto_registry()
+{
+    static auto* v = new std::vector<AutoEntry>;
+    return *v;
+}
+
 struct AutoState {
     int depth = 0;
     bool draining = false;
     int enabled = -1;   // -1: from $WSG_AUTO_BATCH on first use
     size_t max_frames = size_t(1) << 20;
     uint64_t max_bytes = uint64_t(64) << 20;
-    WSReceiveBatch rx{nullptr};
-    WSSendBatch tx{nullptr};
+    std::shared_ptr<WSReceiveBatch> rx_ = std::make_shared<WSReceiveBatch>(nullptr);
+    std::shared_ptr<WSSendBatch> tx_ = std::make_shared<WSSendBatch>(nullptr);
+    WSReceiveBatch& rx = *rx_;
+    WSSendBatch& tx = *tx_;
+    AutoState()
+    {
+        std::lock_guard<std::mutex> g(auto_registry_lock());
+        auto& reg = auto_registry();
+        reg.erase(std::remove_if(reg.begin(), reg.end(), [](const AutoEntry& e) { return e.rx.expired(); }),
+                  reg.end());
+        reg.push_back(AutoEntry{rx_, tx_});
+    }
 };
 
 AutoState& auto_state()
@@ -590,6 +666,23 @@ BatchScope::~BatchScope()
         }
     }
     --st.depth;
+}
+
+void BatchScope::ForgetEverywhere(WebSocket& ws, Transport& transport)
+{
+    std::vector<std::pair<std::shared_ptr<WSReceiveBatch>, std::shared_ptr<WSSendBatch>>> live;
+    {
+        std::lock_guard<std::mutex> g(auto_registry_lock());
+        for (const AutoEntry& e : auto_registry())
+            live.emplace_back(e.rx.lock(), e.tx.lock());
+    }
+    // outside the registry lock: a Forget may wait for a flush on another thread
+    for (auto& [rx, tx] : live) {
+        if (rx)
+            rx->Forget(ws);
+        if (tx)
+            tx->Forget(transport);
+    }
 }
 
 void BatchScope::AtEnd(void* key, void (*fn)(void*))

@@ -27,7 +27,13 @@ struct wsg_ctx {
     hipStream_t stream = nullptr;
     int num_cus = 256;
     int blocks_per_cu = 32;       // encode / fan-out / xor grids
-    int enc_blocks_per_cu = 1024; // k_encode_mask grid, ~1-2 pieces per wave (tools/tune_enc.py: C5 share -15 %, C3-like -6 % vs 32)
+    // k_encode_mask grid: one wave per piece up to 2^31 threads (137 GB of
+    // frames), grid-stride beyond.  A grid capped at 1024 blocks/CU dealt C5's
+    // 5.2 M pieces five per wave, grid-stride, so resident waves streamed five
+    // regions GiB apart: 6.12 vs 5.43 ms for the 16 GiB job (tools/enc_ab.py,
+    // round 3); at or under a grid's worth of pieces the two are the same
+    int enc_blocks_per_cu = 32768;
+    uint64_t enc_launch_pieces = 0;   // k_encode_mask: pieces per launch (0: all in one)
     uint64_t xor_direct_max = 64 << 10;   // per-call XOR: kernel on the pinned stage up to this size (A/B: $WSG_XOR_DIRECT_MAX)
     int dec_tiles_per_block = 0;   // 0: grid from dec_blocks_per_cu alone; k: ceil(tiles / k) blocks (A/B)
     bool check = false;            // $WSG_CHECK=1: operand ranges validated before every device launch (debug)
@@ -305,9 +311,11 @@ int wsg_create(int device, wsg_ctx** out)
         c->check = *e == '1';
     if (const char* e = std::getenv("WSG_ENC_BLOCKS_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
         const int v = std::atoi(e);
-        if (v > 0 && v <= 4096)
+        if (v > 0 && v <= 32768)
             c->enc_blocks_per_cu = v;
     }
+    if (const char* e = std::getenv("WSG_ENC_LAUNCH_PIECES"))   // A/B measurements (tools/c5_split.py)
+        c->enc_launch_pieces = std::strtoull(e, nullptr, 10);
     if (const char* e = std::getenv("WSG_FAN_WAVES_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
         const int v = std::atoi(e);
         if (v > 0 && v <= 64)
@@ -473,9 +481,15 @@ int encode_launch(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, const wsg
     const uint64_t pieces_cap = pieces_bound(n, wire_cap);
     WSG_HIP(wsg::launch_encode_scan(s, d_desc, n, d_wire_off, e.d_piece_start, e.d_scan, e.d_piece_frame, pieces_cap,
                                     wire_cap, err));
+    // one launch per run of at most enc_launch_pieces pieces (0: one launch)
+    const uint64_t per = c->enc_launch_pieces ? c->enc_launch_pieces : pieces_cap;
     const int t = timing_begin(c, s);
-    WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, ceil_div(pieces_cap, wsg::BLOCK / 64), c->enc_blocks_per_cu), d_payload, d_desc, n,
-                                    d_wire_off, e.d_piece_start, e.d_piece_frame, d_wire, wire_cap));
+    for (uint64_t q0 = 0; q0 < pieces_cap; q0 += per) {
+        const uint64_t q1 = std::min<uint64_t>(pieces_cap, q0 + per);
+        WSG_HIP(wsg::launch_encode_mask(s, grid_for(c, ceil_div(q1 - q0, wsg::BLOCK / 64), c->enc_blocks_per_cu),
+                                        d_payload, d_desc, n, d_wire_off, e.d_piece_start, e.d_piece_frame, d_wire,
+                                        wire_cap, uint32_t(q0), uint32_t(q1)));
+    }
     timing_end(c, s, t);
     return WSG_OK;
 }

@@ -63,7 +63,7 @@ hipError_t launch_encode_scan(hipStream_t s, const wsg_send_desc* desc, uint32_t
                               uint64_t wire_cap, unsigned long long* err);
 hipError_t launch_encode_mask(hipStream_t s, int grid, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
                               const uint64_t* wire_off, const uint32_t* piece_start, const uint32_t* piece_frame,
-                              uint8_t* wire, uint64_t wire_cap);
+                              uint8_t* wire, uint64_t wire_cap, uint32_t q_begin, uint32_t q_end);
 // Small-frame batch encode: block-local sizes scan (scan: ceil(n /
 // SCAN_ITEMS) block totals), then k_encode_small, which adds the block
 // prefixes, writes the final wire_off[0..n] and latches capacity errors.
@@ -87,10 +87,12 @@ hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64
                          uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire);
 hipError_t launch_xor(hipStream_t s, int grid, const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,
                       uint32_t phase);
-// Multi-GPU gather (wsg_mgpu.cpp): out_off[g] = stage[g] - stage[first frame of
-// g's chunk] + goff[chunk]; out_off[n_total] = total.
-hipError_t launch_rebase_offsets(hipStream_t s, const uint64_t* stage, const uint64_t* goff, uint64_t n_total,
-                                 uint32_t chunk, uint64_t* out_off, uint64_t total);
+// Multi-GPU gather (wsg_mgpu.cpp): the job's wire offsets from the ranks'
+// local offsets, staged rank by rank at rank_base[r] (chunk c of the job is
+// rank c % world's local chunk c / world, placed at goff[c]);
+// out_off[n_total] = total.
+hipError_t launch_rebase_offsets(hipStream_t s, const uint64_t* stage, const uint64_t* goff, const uint64_t* rank_base,
+                                 uint64_t n_total, uint32_t chunk, uint32_t world, uint64_t* out_off, uint64_t total);
 
 // HIP device a context is bound to (wsg_capi.hip)
 int ctx_device(const wsg_ctx* c);

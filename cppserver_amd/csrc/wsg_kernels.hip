@@ -1107,11 +1107,13 @@ __global__ __launch_bounds__(BLOCK) void k_encode_mask(const uint8_t* __restrict
                                                        const uint64_t* __restrict__ wire_off,
                                                        const uint32_t* __restrict__ piece_start,
                                                        const uint32_t* __restrict__ piece_frame,
-                                                       uint8_t* __restrict__ wire, uint64_t wire_cap)
+                                                       uint8_t* __restrict__ wire, uint64_t wire_cap,
+                                                       uint32_t q_begin, uint32_t q_end)
 {
     if (wire_off[n] > wire_cap)
         return;   // capacity error latched by k_encode_finalize
-    const uint32_t pieces = piece_start[n];
+    // this launch's pieces: [q_begin, min(all pieces, q_end))
+    const uint32_t pieces = min(piece_start[n], q_end);
     const uint32_t waves = gridDim.x * (BLOCK / 64);
     // Software pipeline over the wave's pieces: while piece q streams, the
     // descriptor of piece q + W (frame index already known) and the frame
@@ -1123,7 +1125,7 @@ __global__ __launch_bounds__(BLOCK) void k_encode_mask(const uint8_t* __restrict
         uint32_t ps;
     };
     auto meta = [&](uint32_t i) { return Meta{load_desc(desc + i), wire_off[i], piece_start[i]}; };
-    uint32_t q = blockIdx.x * (BLOCK / 64) + wave_id();
+    uint32_t q = q_begin + blockIdx.x * (BLOCK / 64) + wave_id();
     if (q >= pieces)
         return;
     Meta cur = meta(piece_frame[q]);
@@ -1755,9 +1757,10 @@ hipError_t launch_encode_scan(hipStream_t s, const wsg_send_desc* desc, uint32_t
 
 hipError_t launch_encode_mask(hipStream_t s, int grid, const uint8_t* payload, const wsg_send_desc* desc, uint32_t n,
                               const uint64_t* wire_off, const uint32_t* piece_start, const uint32_t* piece_frame,
-                              uint8_t* wire, uint64_t wire_cap)
+                              uint8_t* wire, uint64_t wire_cap, uint32_t q_begin, uint32_t q_end)
 {
-    k_encode_mask<<<grid, BLOCK, 0, s>>>(payload, desc, n, wire_off, piece_start, piece_frame, wire, wire_cap);
+    k_encode_mask<<<grid, BLOCK, 0, s>>>(payload, desc, n, wire_off, piece_start, piece_frame, wire, wire_cap, q_begin,
+                                         q_end);
     return hipGetLastError();
 }
 
@@ -1861,25 +1864,33 @@ bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_
 
 // The job's wire offsets on the gather root: every chunk's frame offsets
 // arrive relative to its sender's local wire.
+// Multi-GPU gather root: the job's wire offsets from every rank's local
+// frame offsets.  stage holds rank r's n_local(r) local offsets at
+// [rank_base[r], rank_base[r + 1]) (one transfer per rank); global frame g
+// is in chunk c = g / chunk, owned by rank c % world as its local chunk
+// q = c / world, which the gather placed at goff[c] in the job's wire.
 __global__ __launch_bounds__(BLOCK) void k_rebase_offsets(const uint64_t* __restrict__ stage,
-                                                          const uint64_t* __restrict__ goff, uint64_t n_total,
-                                                          uint32_t chunk, uint64_t* __restrict__ out_off,
+                                                          const uint64_t* __restrict__ goff,
+                                                          const uint64_t* __restrict__ rank_base, uint64_t n_total,
+                                                          uint32_t chunk, uint32_t world, uint64_t* __restrict__ out_off,
                                                           uint64_t total)
 {
     const uint64_t stride = uint64_t(gridDim.x) * BLOCK;
     for (uint64_t g = uint64_t(blockIdx.x) * BLOCK + threadIdx.x; g < n_total; g += stride) {
         const uint64_t c = g / chunk;
-        out_off[g] = stage[g] - stage[c * chunk] + goff[c];
+        const uint64_t r = c % world, q = c / world;
+        const uint64_t* loc = stage + rank_base[r] + q * chunk;
+        out_off[g] = loc[g - c * chunk] - loc[0] + goff[c];
     }
     if (blockIdx.x == 0 && threadIdx.x == 0)
         out_off[n_total] = total;
 }
 
-hipError_t launch_rebase_offsets(hipStream_t s, const uint64_t* stage, const uint64_t* goff, uint64_t n_total,
-                                 uint32_t chunk, uint64_t* out_off, uint64_t total)
+hipError_t launch_rebase_offsets(hipStream_t s, const uint64_t* stage, const uint64_t* goff, const uint64_t* rank_base,
+                                 uint64_t n_total, uint32_t chunk, uint32_t world, uint64_t* out_off, uint64_t total)
 {
     const uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>((n_total + BLOCK - 1) / BLOCK, 1), 8192);
-    k_rebase_offsets<<<uint32_t(blocks), BLOCK, 0, s>>>(stage, goff, n_total, chunk, out_off, total);
+    k_rebase_offsets<<<uint32_t(blocks), BLOCK, 0, s>>>(stage, goff, rank_base, n_total, chunk, world, out_off, total);
     return hipGetLastError();
 }
 

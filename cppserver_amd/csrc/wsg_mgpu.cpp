@@ -120,11 +120,13 @@ struct Local {
     ncclComm_t comm = nullptr;
     uint64_t* d_sizes = nullptr;   // this rank's chunk sizes | every rank's (all-gather)
     uint64_t sizes_cap = 0;
-    uint64_t* d_stage = nullptr;   // root: gathered local frame offsets (n_total)
+    uint64_t* d_status = nullptr;  // rank form: status all-gather (1 + world words, made at create)
+    uint64_t* d_stage = nullptr;   // root: every rank's local frame offsets, rank by rank (n_total)
     uint64_t stage_cap = 0;
-    uint64_t* d_goff = nullptr;    // root: global offset of every chunk
+    uint64_t* d_goff = nullptr;    // root: global offset of every chunk, then every rank's stage base
     uint64_t goff_cap = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;   // encode start/end, gather end/start
+    hipEvent_t done = nullptr;     // one-process form: this rank's transfers to the root are queued before it
 };
 
 template <class T>
@@ -225,6 +227,11 @@ inline bool frame_status(int rc) { return rc == WSG_OK || rc == WSG_EINVAL || rc
 
 struct wsg_mgpu {
     int world = 0;
+    // wsg_mgpu_create: every rank lives in this process (one or more per
+    // device): the exchange is host bookkeeping plus device copies (xGMI
+    // peer copies between GPUs, plain copies within one); wsg_mgpu_create_rank:
+    // one rank here, the others in their processes, over RCCL
+    bool all_local = false;
     std::vector<Local> local;   // ranks driven by this process
 };
 
@@ -265,9 +272,10 @@ int wsg_mgpu_destroy(wsg_mgpu* g)
         if (l.comm && r)
             r->CommDestroy(l.comm);
         (void)hipFree(l.d_sizes);
+        (void)hipFree(l.d_status);
         (void)hipFree(l.d_stage);
         (void)hipFree(l.d_goff);
-        for (hipEvent_t e : {l.e0, l.e1, l.e2, l.e3})
+        for (hipEvent_t e : {l.e0, l.e1, l.e2, l.e3, l.done})
             if (e)
                 (void)hipEventDestroy(e);
         if (l.ctx)
@@ -287,8 +295,30 @@ int init_locals(wsg_mgpu* g)
         WSG_HIP(hipSetDevice(l.device));
         for (hipEvent_t* e : {&l.e0, &l.e1, &l.e2, &l.e3})
             WSG_HIP(hipEventCreate(e));
+        WSG_HIP(hipEventCreateWithFlags(&l.done, hipEventDisableTiming));
+        // the status exchange must never fail to allocate (every rank has
+        // to reach it, whatever went wrong before)
+        if (hipMalloc(&l.d_status, (uint64_t(g->world) + 1) * sizeof(uint64_t)) != hipSuccess)
+            return WSG_ENOMEM;
     }
     return WSG_OK;
+}
+
+// direct xGMI access between every two distinct devices of the group, where
+// the platform offers it (hipMemcpyPeerAsync works either way)
+void enable_peers(const int* devices, int ndev)
+{
+    for (int i = 0; i < ndev; ++i)
+        for (int j = 0; j < ndev; ++j) {
+            if (devices[i] == devices[j])
+                continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, devices[i], devices[j]) != hipSuccess || !can)
+                continue;
+            if (hipSetDevice(devices[i]) == hipSuccess)
+                (void)hipDeviceEnablePeerAccess(devices[j], 0);   // "already enabled" is fine
+            (void)hipGetLastError();
+        }
 }
 
 } // namespace
@@ -298,13 +328,17 @@ int wsg_mgpu_create(const int* devices, int ndev, wsg_mgpu** out)
     if (!out || !devices || ndev <= 0)
         return WSG_EINVAL;
     *out = nullptr;
-    const Rccl* r = rccl();
-    if (!r)
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess)
         return WSG_EHIP;
+    for (int i = 0; i < ndev; ++i)
+        if (devices[i] < 0 || devices[i] >= count)
+            return WSG_EINVAL;
     wsg_mgpu* g = new (std::nothrow) wsg_mgpu();
     if (!g)
         return WSG_ENOMEM;
     g->world = ndev;
+    g->all_local = true;   // a device may be listed more than once: one rank each
     g->local.resize(size_t(ndev));
     for (int i = 0; i < ndev; ++i) {
         g->local[size_t(i)].device = devices[i];
@@ -314,13 +348,7 @@ int wsg_mgpu_create(const int* devices, int ndev, wsg_mgpu** out)
         wsg_mgpu_destroy(g);
         return rc;
     }
-    std::vector<ncclComm_t> comms(size_t(ndev), nullptr);
-    if (r->CommInitAll(comms.data(), ndev, devices) != ncclSuccess) {
-        wsg_mgpu_destroy(g);
-        return WSG_EHIP;
-    }
-    for (int i = 0; i < ndev; ++i)
-        g->local[size_t(i)].comm = comms[size_t(i)];
+    enable_peers(devices, ndev);
     *out = g;
     return WSG_OK;
 }
@@ -393,8 +421,9 @@ int encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* 
     if (!g || chunk == 0 || root < 0 || root >= g->world || !n_local || !d_wire || !wire_cap || !d_wire_off ||
         !d_payload || !d_desc)
         return WSG_EINVAL;
-    const Rccl* r = rccl();
-    if (!r)
+    const bool all_local = g->all_local;
+    const Rccl* r = all_local ? nullptr : rccl();
+    if (!all_local && !r)
         return WSG_EHIP;
     const int world = g->world;
     const size_t nl = g->local.size();
@@ -410,162 +439,218 @@ int encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* 
     }
     const uint64_t n_chunks = ceil_div(n_total, chunk);
     const uint64_t maxq = ceil_div(n_chunks, uint64_t(world));   // chunks per rank, at most
+    auto stream_of = [](const Local& l) { return static_cast<hipStream_t>(wsg_stream(l.ctx)); };
+
+    // In the rank-per-process form every rank must reach every collective
+    // below, whatever failed locally: local failures go into `status`, which
+    // the ranks exchange (exchange_status) before anything depends on it.
+    int status = WSG_OK;
+    auto fail = [&](int rc) {
+        if (rc && !status)
+            status = rc;
+    };
+    auto exchange_status = [&]() -> int {
+        if (all_local)
+            return status;
+        for (Local& l : g->local) {
+            WSG_HIP(hipSetDevice(l.device));
+            const uint64_t mine = uint64_t(uint32_t(-status));
+            WSG_HIP(hipMemcpy(l.d_status, &mine, sizeof(uint64_t), hipMemcpyHostToDevice));
+        }
+        WSG_NCCL(r->GroupStart());
+        for (Local& l : g->local)
+            WSG_NCCL(r->AllGather(l.d_status, l.d_status + 1, 1, ncclUint64, l.comm, stream_of(l)));
+        WSG_NCCL(r->GroupEnd());
+        std::vector<uint64_t> st(uint64_t(world), 0);
+        Local& l = g->local[0];
+        WSG_HIP(hipSetDevice(l.device));
+        WSG_HIP(hipStreamSynchronize(stream_of(l)));
+        WSG_HIP(hipMemcpy(st.data(), l.d_status + 1, st.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        for (uint64_t e : st)
+            if (e && !status)
+                status = -int(e);
+        return status;
+    };
+
     Local* root_l = nullptr;
+    std::vector<bool> ok(nl, true);
     for (size_t i = 0; i < nl; ++i) {
         Local& l = g->local[i];
-        if (uint64_t(n_local[i]) != shard_count(n_total, chunk, world, l.rank))
-            return WSG_EINVAL;   // not this rank's round-robin share of the job
+        if (uint64_t(n_local[i]) != shard_count(n_total, chunk, world, l.rank)) {
+            fail(WSG_EINVAL);   // not this rank's round-robin share of the job
+            ok[i] = false;
+        }
         if (l.rank == root) {
             root_l = &l;
             if (!d_out)
-                return WSG_EINVAL;
+                fail(WSG_EINVAL);
         }
     }
 
     // 1. every local rank encodes its shard (concurrently, one stream each)
     for (size_t i = 0; i < nl; ++i) {
         Local& l = g->local[i];
-        WSG_HIP(hipSetDevice(l.device));
-        hipStream_t s = static_cast<hipStream_t>(wsg_stream(l.ctx));
-        WSG_HIP(hipEventRecord(l.e0, s));
+        if (!ok[i] || hipSetDevice(l.device) != hipSuccess) {
+            fail(WSG_EINVAL);
+            ok[i] = false;
+            continue;
+        }
+        hipStream_t s = stream_of(l);
+        if (hipEventRecord(l.e0, s) != hipSuccess)
+            fail(WSG_EHIP);
         if (int rc = wsg_encode_batch(l.ctx, d_payload[i], d_desc[i], n_local[i], d_wire[i], wire_cap[i],
-                                      d_wire_off[i], s))
-            return rc;
-        WSG_HIP(hipEventRecord(l.e1, s));
+                                      d_wire_off[i], s)) {
+            fail(rc);
+            ok[i] = false;
+        }
+        if (hipEventRecord(l.e1, s) != hipSuccess)
+            fail(WSG_EHIP);
     }
-    // 2. chunk byte sizes of every local rank (host), then all ranks' sizes
+    // 2. each local rank's frame offsets and chunk byte sizes (host); the
+    // buffers the exchange needs are made before the status round
     std::vector<std::vector<uint64_t>> loff(nl);
-    std::vector<uint64_t> send(maxq);
-    int status = WSG_OK;
+    std::vector<std::vector<uint64_t>> sizes(nl, std::vector<uint64_t>(maxq, 0));
     for (size_t i = 0; i < nl; ++i) {
         Local& l = g->local[i];
-        WSG_HIP(hipSetDevice(l.device));
-        hipStream_t s = static_cast<hipStream_t>(wsg_stream(l.ctx));
-        if (int rc = wsg_sync(l.ctx, s))
-            status = status ? status : rc;   // keep the collectives matched across ranks
-        loff[i].resize(size_t(n_local[i]) + 1);
-        WSG_HIP(hipMemcpy(loff[i].data(), d_wire_off[i], loff[i].size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
-        std::fill(send.begin(), send.end(), 0);
+        loff[i].assign(size_t(n_local[i]) + 1, 0);
+        if (!ok[i] || hipSetDevice(l.device) != hipSuccess)
+            continue;
+        if (int rc = wsg_sync(l.ctx, stream_of(l))) {
+            fail(rc);
+            continue;
+        }
+        if (hipMemcpy(loff[i].data(), d_wire_off[i], loff[i].size() * sizeof(uint64_t), hipMemcpyDeviceToHost) !=
+            hipSuccess) {
+            fail(WSG_EHIP);
+            continue;
+        }
         for (uint64_t q = 0; q * chunk < n_local[i]; ++q)
-            send[q] = loff[i][std::min<uint64_t>((q + 1) * chunk, n_local[i])] - loff[i][q * chunk];
-        if (int rc = grow(l.d_sizes, l.sizes_cap, maxq * (uint64_t(world) + 1)))
-            return rc;
-        WSG_HIP(hipMemcpy(l.d_sizes, send.data(), maxq * sizeof(uint64_t), hipMemcpyHostToDevice));
+            sizes[i][q] = loff[i][std::min<uint64_t>((q + 1) * chunk, n_local[i])] - loff[i][q * chunk];
+        if (!all_local)
+            fail(grow(l.d_sizes, l.sizes_cap, maxq * (uint64_t(world) + 1)));
+        if (l.rank == root) {
+            fail(grow(l.d_stage, l.stage_cap, n_total));
+            fail(grow(l.d_goff, l.goff_cap, n_chunks + 1 + uint64_t(world) + 1));
+        }
     }
-    WSG_NCCL(r->GroupStart());
-    for (size_t i = 0; i < nl; ++i) {
-        Local& l = g->local[i];
-        WSG_NCCL(r->AllGather(l.d_sizes, l.d_sizes + maxq, maxq, ncclUint64, l.comm,
-                              static_cast<hipStream_t>(wsg_stream(l.ctx))));
-    }
-    WSG_NCCL(r->GroupEnd());
-    std::vector<uint64_t> all(maxq * uint64_t(world));
-    {
-        Local& l = g->local[0];
-        WSG_HIP(hipSetDevice(l.device));
-        WSG_HIP(hipStreamSynchronize(static_cast<hipStream_t>(wsg_stream(l.ctx))));
-        WSG_HIP(hipMemcpy(all.data(), l.d_sizes + maxq, all.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    }
-    // 3. the job's chunk offsets (global chunk order)
-    std::vector<uint64_t> goff(n_chunks + 1, 0);
-    for (uint64_t c = 0; c < n_chunks; ++c)
-        goff[c + 1] = goff[c] + all[(c % uint64_t(world)) * maxq + c / uint64_t(world)];
-    const uint64_t total = goff[n_chunks];
-    if (root_l && total > out_cap)
-        status = status ? status : WSG_ENOMEM;
-    // an encode error or a short root buffer on any rank must stop every
-    // rank before the transfers, or the others would wait for it: the
-    // status goes round in a second all-gather
-    {
-        std::vector<uint64_t> st(uint64_t(world), 0);
+    if (exchange_status())
+        return status;
+
+    // 3. every rank's chunk sizes -> the job's chunk offsets (global order)
+    std::vector<uint64_t> all(maxq * uint64_t(world), 0);
+    if (all_local) {
+        for (size_t i = 0; i < nl; ++i)
+            std::copy(sizes[i].begin(), sizes[i].end(), all.begin() + ptrdiff_t(uint64_t(g->local[i].rank) * maxq));
+    } else {
         for (size_t i = 0; i < nl; ++i) {
             Local& l = g->local[i];
             WSG_HIP(hipSetDevice(l.device));
-            const uint64_t mine = uint64_t(uint32_t(-status));
-            WSG_HIP(hipMemcpy(l.d_sizes, &mine, sizeof(uint64_t), hipMemcpyHostToDevice));
+            WSG_HIP(hipMemcpy(l.d_sizes, sizes[i].data(), maxq * sizeof(uint64_t), hipMemcpyHostToDevice));
         }
         WSG_NCCL(r->GroupStart());
-        for (size_t i = 0; i < nl; ++i) {
-            Local& l = g->local[i];
-            WSG_NCCL(r->AllGather(l.d_sizes, l.d_sizes + maxq, 1, ncclUint64, l.comm,
-                                  static_cast<hipStream_t>(wsg_stream(l.ctx))));
-        }
+        for (Local& l : g->local)
+            WSG_NCCL(r->AllGather(l.d_sizes, l.d_sizes + maxq, maxq, ncclUint64, l.comm, stream_of(l)));
         WSG_NCCL(r->GroupEnd());
         Local& l = g->local[0];
         WSG_HIP(hipSetDevice(l.device));
-        WSG_HIP(hipStreamSynchronize(static_cast<hipStream_t>(wsg_stream(l.ctx))));
-        WSG_HIP(hipMemcpy(st.data(), l.d_sizes + maxq, st.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
-        for (uint64_t e : st)
-            if (e && !status)
-                status = -int(e);
+        WSG_HIP(hipStreamSynchronize(stream_of(l)));
+        WSG_HIP(hipMemcpy(all.data(), l.d_sizes + maxq, all.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
     }
-    if (status)
+    // goff[c]: where chunk c goes in the root's output; then every rank's
+    // base in the root's offset stage (its frames, rank by rank)
+    std::vector<uint64_t> goff(n_chunks + 1 + uint64_t(world) + 1, 0);
+    for (uint64_t c = 0; c < n_chunks; ++c)
+        goff[c + 1] = goff[c] + all[(c % uint64_t(world)) * maxq + c / uint64_t(world)];
+    const uint64_t total = goff[n_chunks];
+    uint64_t* rank_base = goff.data() + n_chunks + 1;
+    for (int k = 0; k < world; ++k)
+        rank_base[k + 1] = rank_base[k] + shard_count(n_total, chunk, world, k);
+    if (root_l && total > out_cap)
+        fail(WSG_ENOMEM);
+    if (root_l && !status) {
+        if (hipSetDevice(root_l->device) != hipSuccess ||
+            hipMemcpy(root_l->d_goff, goff.data(), goff.size() * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess)
+            fail(WSG_EHIP);
+    }
+    // a short root buffer must stop every rank before the transfers, or the
+    // others would wait for it
+    if (exchange_status())
         return status;
 
-    // 4. one grouped transfer: each chunk to its place in the root's output,
-    // with its frame offsets
-    if (root_l) {
-        WSG_HIP(hipSetDevice(root_l->device));
-        // the senders always send their chunks' frame offsets (8 B a frame):
-        // they cannot know whether the root wants them
-        if (int rc = grow(root_l->d_stage, root_l->stage_cap, n_total))
-            return rc;
-        if (int rc = grow(root_l->d_goff, root_l->goff_cap, n_chunks + 1))
-            return rc;
-        WSG_HIP(hipMemcpy(root_l->d_goff, goff.data(), goff.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-    }
-    for (size_t i = 0; i < nl; ++i) {
-        Local& l = g->local[i];
+    // 4. the transfers: every chunk straight to its place in the root's
+    // output; every rank's frame offsets in one piece to the root's stage.
+    // Per group: one data transfer per chunk (the output is in job order, a
+    // rank's chunks are not adjacent there) + one offsets transfer per rank.
+    for (Local& l : g->local) {
         WSG_HIP(hipSetDevice(l.device));
-        WSG_HIP(hipEventRecord(l.e3, static_cast<hipStream_t>(wsg_stream(l.ctx))));
+        WSG_HIP(hipEventRecord(l.e3, stream_of(l)));
     }
-    WSG_NCCL(r->GroupStart());
-    for (size_t i = 0; i < nl; ++i) {
-        Local& l = g->local[i];
-        hipStream_t s = static_cast<hipStream_t>(wsg_stream(l.ctx));
-        for (uint64_t c = uint64_t(l.rank), q = 0; c < n_chunks; c += uint64_t(world), ++q) {
-            const uint64_t lo = loff[i][q * chunk];
-            const uint64_t bytes = goff[c + 1] - goff[c];
-            const uint64_t frames = std::min<uint64_t>(chunk, n_local[i] - q * chunk);
+    if (all_local) {
+        const int rdev = root_l->device;
+        for (size_t i = 0; i < nl; ++i) {
+            Local& l = g->local[i];
+            hipStream_t s = stream_of(l);
+            WSG_HIP(hipSetDevice(l.device));
+            auto copy = [&](void* dst, const void* src, uint64_t bytes) -> hipError_t {
+                if (!bytes)
+                    return hipSuccess;
+                return l.device == rdev ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s)
+                                        : hipMemcpyPeerAsync(dst, rdev, src, l.device, bytes, s);
+            };
+            for (uint64_t c = uint64_t(l.rank), q = 0; c < n_chunks; c += uint64_t(world), ++q)
+                WSG_HIP(copy(d_out + goff[c], d_wire[i] + loff[i][q * chunk], goff[c + 1] - goff[c]));
+            WSG_HIP(copy(root_l->d_stage + rank_base[l.rank], d_wire_off[i], uint64_t(n_local[i]) * sizeof(uint64_t)));
+            WSG_HIP(hipEventRecord(l.done, s));
+        }
+        WSG_HIP(hipSetDevice(rdev));
+        for (Local& l : g->local)   // the root's stream goes on once every rank's copies are done
+            if (&l != root_l)
+                WSG_HIP(hipStreamWaitEvent(stream_of(*root_l), l.done, 0));
+    } else {
+        WSG_NCCL(r->GroupStart());
+        for (size_t i = 0; i < nl; ++i) {
+            Local& l = g->local[i];
+            hipStream_t s = stream_of(l);
             if (l.rank == root) {
-                if (bytes)
-                    WSG_HIP(hipMemcpyAsync(d_out + goff[c], d_wire[i] + lo, bytes, hipMemcpyDeviceToDevice, s));
-                WSG_HIP(hipMemcpyAsync(root_l->d_stage + c * chunk, d_wire_off[i] + q * chunk,
-                                       frames * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+                for (uint64_t c = uint64_t(l.rank), q = 0; c < n_chunks; c += uint64_t(world), ++q)
+                    if (goff[c + 1] > goff[c])
+                        WSG_HIP(hipMemcpyAsync(d_out + goff[c], d_wire[i] + loff[i][q * chunk], goff[c + 1] - goff[c],
+                                               hipMemcpyDeviceToDevice, s));
+                if (n_local[i])
+                    WSG_HIP(hipMemcpyAsync(root_l->d_stage + rank_base[l.rank], d_wire_off[i],
+                                           uint64_t(n_local[i]) * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+                for (uint64_t c = 0; c < n_chunks; ++c) {
+                    const int owner = int(c % uint64_t(world));
+                    if (owner != root && goff[c + 1] > goff[c])
+                        WSG_NCCL(r->Recv(d_out + goff[c], goff[c + 1] - goff[c], ncclUint8, owner, l.comm, s));
+                }
+                for (int k = 0; k < world; ++k)
+                    if (k != root && rank_base[k + 1] > rank_base[k])
+                        WSG_NCCL(r->Recv(root_l->d_stage + rank_base[k], rank_base[k + 1] - rank_base[k], ncclUint64, k,
+                                         l.comm, s));
                 continue;
             }
-            if (bytes)
-                WSG_NCCL(r->Send(d_wire[i] + lo, bytes, ncclUint8, root, l.comm, s));
-            WSG_NCCL(r->Send(d_wire_off[i] + q * chunk, frames, ncclUint64, root, l.comm, s));
+            for (uint64_t c = uint64_t(l.rank), q = 0; c < n_chunks; c += uint64_t(world), ++q)
+                if (goff[c + 1] > goff[c])
+                    WSG_NCCL(r->Send(d_wire[i] + loff[i][q * chunk], goff[c + 1] - goff[c], ncclUint8, root, l.comm, s));
+            if (n_local[i])
+                WSG_NCCL(r->Send(d_wire_off[i], n_local[i], ncclUint64, root, l.comm, s));
         }
-        if (l.rank != root)
-            continue;
-        for (uint64_t c = 0; c < n_chunks; ++c) {
-            const int owner = int(c % uint64_t(world));
-            if (owner == root)
-                continue;
-            const uint64_t bytes = goff[c + 1] - goff[c];
-            const uint64_t frames = std::min<uint64_t>(chunk, n_total - c * chunk);
-            if (bytes)
-                WSG_NCCL(r->Recv(d_out + goff[c], bytes, ncclUint8, owner, l.comm, s));
-            WSG_NCCL(r->Recv(root_l->d_stage + c * chunk, frames, ncclUint64, owner, l.comm, s));
-        }
+        WSG_NCCL(r->GroupEnd());
     }
-    WSG_NCCL(r->GroupEnd());
     if (root_l) {
-        hipStream_t s = static_cast<hipStream_t>(wsg_stream(root_l->ctx));
+        hipStream_t s = stream_of(*root_l);
         WSG_HIP(hipSetDevice(root_l->device));
         if (d_out_off)
-            WSG_HIP(wsg::launch_rebase_offsets(s, root_l->d_stage, root_l->d_goff, n_total, chunk, d_out_off, total));
+            WSG_HIP(wsg::launch_rebase_offsets(s, root_l->d_stage, root_l->d_goff, root_l->d_goff + n_chunks + 1,
+                                               n_total, chunk, uint32_t(world), d_out_off, total));
     }
-    for (size_t i = 0; i < nl; ++i) {
-        Local& l = g->local[i];
+    for (Local& l : g->local) {
         WSG_HIP(hipSetDevice(l.device));
-        WSG_HIP(hipEventRecord(l.e2, static_cast<hipStream_t>(wsg_stream(l.ctx))));
+        WSG_HIP(hipEventRecord(l.e2, stream_of(l)));
     }
     double enc = 0.0, gat = 0.0;
-    for (size_t i = 0; i < nl; ++i) {
-        Local& l = g->local[i];
+    for (Local& l : g->local) {
         WSG_HIP(hipSetDevice(l.device));
         WSG_HIP(hipEventSynchronize(l.e2));
         float a = 0.f, b = 0.f;

@@ -19,7 +19,11 @@
  * may come from any thread (a mutex guards the queue, as the reference's
  * per-session strands and locks let any IO thread call in); a Flush runs on
  * the calling thread with that thread's GPU codec context unless the batch
- * was given one, and fires the callbacks on that thread.
+ * was given one, and fires the callbacks on that thread.  Forget(ws) from
+ * another thread while a flush is delivering waits until the flush has
+ * dropped ws's remaining frames (after the callback it may be running for
+ * ws returns), so ws can be destroyed as soon as Forget returns; from
+ * inside a callback of the flush it takes effect at once.
  */
 #ifndef CPPSERVER_AMD_WS_BATCH_H
 #define CPPSERVER_AMD_WS_BATCH_H
@@ -27,10 +31,13 @@
 #include "server/ws/ws.h"
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <thread>
+#include <utility>
 #include <vector>
 
 namespace CppServer {
@@ -100,15 +107,20 @@ private:
     };
 
     void Emit(WebSocket& ws, const uint8_t* frame, uint64_t total, uint32_t hdr, const uint8_t* key);
+    void ApplyPending(size_t from);
     static void Grow(Pinned& b, uint64_t need);
     static void Release(Pinned& b);
 
     wsg_ctx* _ctx;
     std::vector<wsg_ctx*> _devs;   // SetDevices: owned, one per device
-    Batch _cur, _spare;
+    Batch _cur, _spare;   // queueing | the flush's (its records: written by the flushing thread only)
     bool _flushing = false;
-    mutable std::mutex _lock;   // _cur, the records of _spare, _flushing
-    std::atomic<uint64_t> _forgets{0};   // Forget() calls: a flush re-reads its records after one
+    std::thread::id _flusher;
+    std::vector<WebSocket*> _pending;    // other threads' Forget()s the flush has not applied yet
+    std::atomic<bool> _has_pending{false};
+    uint64_t _applied = 0;               // ApplyPending rounds (a waiting Forget returns after the next)
+    std::condition_variable _applied_cv;
+    mutable std::mutex _lock;   // _cur, _flushing, _pending, _applied
 };
 
 class Transport;
@@ -179,6 +191,8 @@ private:
         std::shared_ptr<std::function<void(const uint8_t*, size_t)>> deliver;
     };
     void Push(Rec rec, uint32_t key, uint8_t opcode, bool mask, const void* buffer, size_t size, int status);
+    void ForgetIf(Transport* transport, void* tag);
+    void ApplyPending(size_t from);
 
     struct Queue_ {
         Pinned payload;
@@ -188,12 +202,16 @@ private:
 
     wsg_ctx* _ctx;
     std::vector<wsg_ctx*> _devs;   // SetDevices: owned, one per device
-    Queue_ _q, _inflight;   // frames being queued | the frames a flush is encoding
+    Queue_ _q, _inflight;   // frames being queued | the frames a flush is encoding (written by its thread only)
     Pinned _wire;
     std::vector<uint64_t> _wire_off;
     bool _flushing = false;
-    mutable std::mutex _lock;   // _q, _flushing
-    std::atomic<uint64_t> _forgets{0};   // Forget() calls: a flush re-reads its records after one
+    std::thread::id _flusher;
+    std::vector<std::pair<Transport*, void*>> _pending;   // other threads' Forget()s not applied yet
+    std::atomic<bool> _has_pending{false};
+    uint64_t _applied = 0;
+    std::condition_variable _applied_cv;
+    mutable std::mutex _lock;   // _q, _flushing, _pending, _applied
 };
 
 /*
@@ -242,6 +260,12 @@ public:
     static WSSendBatch& Send();
     //! Early flush when a batch passed the limits (inside a scope)
     static void CheckLimits();
+
+    //! Drop a connection's queued frames from the automatic batches of EVERY
+    //! thread (a session queued into another thread's scope, e.g. a SendAsync
+    //! from a worker thread), waiting for a flush in progress there to drop
+    //! them; the connection's destructor calls it
+    static void ForgetEverywhere(WebSocket& ws, Transport& transport);
 
     //! Call fn(key) once when the outermost scope on this thread ends, after
     //! its last flush (a transport that coalesces what one scope sends: the

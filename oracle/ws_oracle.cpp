@@ -43,6 +43,8 @@ struct Conn {
     // recorded callbacks
     bool record = true;
     std::vector<Event> events;
+    wso_callback cb = nullptr;       // set: callbacks instead of recorded events
+    void* user = nullptr;
     size_t delivered = 0;            // byte counter used by the timing loop
 
     void reset_frame()
@@ -110,6 +112,10 @@ struct Conn {
     void deliver(int kind, const uint8_t* p, size_t n, int status)
     {
         delivered += n;
+        if (cb) {   // the onWS* callback: a borrowed pointer, as the reference hands out
+            cb(user, kind, p, n, status);
+            return;
+        }
         if (record)
             events.push_back(Event{kind, status, std::vector<uint8_t>(p, p + n)});
     }
@@ -336,6 +342,12 @@ extern "C" {
 wso_session* wso_new(void) { return new wso_session(); }
 void wso_free(wso_session* s) { delete s; }
 void wso_set_send_key(wso_session* s, uint32_t key) { set_le32(s->c.skey, key); }
+
+void wso_set_callback(wso_session* s, wso_callback cb, void* user)
+{
+    s->c.cb = cb;
+    s->c.user = user;
+}
 void wso_clear(wso_session* s) { s->c.clear(); }
 
 size_t wso_prepare_send(wso_session* s, uint8_t opcode, int mask, const void* buf, size_t size,

@@ -44,6 +44,11 @@ size_t wso_prepare_send(wso_session* s, uint8_t opcode, int mask,
 const uint8_t* wso_send_buffer(wso_session* s, size_t* len);
 void   wso_prepare_receive(wso_session* s, const void* buf, size_t size); /* ws.cpp:273 */
 size_t wso_required(wso_session* s);                                /* ws.cpp:458 */
+/* Callbacks (ws.cpp:415-452's onWS* calls) instead of recorded events: the
+ * payload pointer is borrowed until the callback returns, as in the
+ * reference.  Used by the CPU-reference echo loop (tools/bench_echo_ref).  */
+typedef void (*wso_callback)(void* user, int kind, const uint8_t* data, size_t len, int status);
+void   wso_set_callback(wso_session* s, wso_callback cb, void* user);
 /* Recorded callbacks (copies of the delivered bytes). */
 size_t wso_event_count(wso_session* s);
 int    wso_event(wso_session* s, size_t i, int* kind, int* status,

@@ -1,0 +1,246 @@
+// test_batch_threads.cpp — the batches across threads (host only, no GPU):
+// one thread flushes (delivering frames to connections, handing frames to
+// transports) while another Forgets and destroys connections and
+// transports; and a connection destroyed on one thread while another
+// thread's BatchScope still holds frames it queued.  Built twice by
+// tests/cpp/Makefile, under ThreadSanitizer and under AddressSanitizer, and
+// run by tests/test_sanitize.py.  Every frame carries key 0 (the server
+// direction, reference ws.cpp:206) or no mask, so no GPU pass runs: the batches
+// frame and hand out the bytes on the host exactly as they do around a GPU pass.
+#include "server/ws/ws_batch.h"
+#include "server/ws/ws_session.h"
+#include "server/ws/ws_transport.h"
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <random>
+#include <thread>
+#include <vector>
+
+using namespace CppServer::WS;
+
+// The batches keep their frames in page-locked memory (wsg_host_alloc, HIP)
+// for the GPU pass; this host-only test has no device, so the executable's
+// own definitions take the place of libwsg.so's (symbol interposition): plain
+// heap memory, which is all a batch needs when no GPU pass runs.
+extern "C" int wsg_host_alloc(size_t bytes, void** out)
+{
+    *out = std::malloc(bytes ? bytes : 1);
+    return *out ? WSG_OK : WSG_ENOMEM;
+}
+extern "C" int wsg_host_free(void* p)
+{
+    std::free(p);
+    return WSG_OK;
+}
+
+static std::atomic<int> g_failures{0}, g_checks{0};
+#define CHECK(cond)                                                                    \
+    do {                                                                               \
+        ++g_checks;                                                                    \
+        if (!(cond)) {                                                                 \
+            ++g_failures;                                                              \
+            std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+        }                                                                              \
+    } while (0)
+
+constexpr uint64_t kAlive = 0xA11CEA11CEA11CEull;
+
+// a connection whose callbacks check it is still alive
+struct Conn : WebSocket {
+    uint64_t magic = kAlive;
+    uint64_t bytes = 0;   // written by the delivering thread only
+    ~Conn() override { magic = 0; }
+
+protected:
+    void onWSReceived(const void* buffer, size_t size) override
+    {
+        CHECK(magic == kAlive);
+        bytes += size;
+        std::this_thread::yield();   // widen the window for the other thread
+    }
+};
+
+// a transport that counts what it is handed, checking it is still alive
+struct Sink : Transport {
+    uint64_t magic = kAlive;
+    std::atomic<uint64_t> bytes{0}, frames{0};
+    ~Sink() override { magic = 0; }
+    size_t Send(const void* b, size_t n) override { return SendAsync(b, n) ? n : 0; }
+    bool SendAsync(const void*, size_t n) override
+    {
+        CHECK(magic == kAlive);
+        bytes += n;
+        ++frames;
+        std::this_thread::yield();
+        return true;
+    }
+    size_t Receive(void*, size_t) override { return 0; }
+    bool Disconnect() override { return true; }
+    bool IsConnected() const override { return true; }
+};
+
+static std::vector<uint8_t> unmasked_frame(size_t len, uint8_t fill)
+{
+    std::vector<uint8_t> f{uint8_t(0x82), uint8_t(len)};
+    f.resize(2 + len, fill);
+    return f;
+}
+
+// One thread feeds and flushes a receive batch; another swaps connections
+// out of the table, Forgets them and deletes them at once.
+static void test_receive_forget_while_flushing()
+{
+    WSReceiveBatch batch(nullptr);
+    std::mutex table_lock;
+    std::vector<Conn*> table;
+    for (int i = 0; i < 12; ++i)
+        table.push_back(new Conn);
+    std::atomic<bool> stop{false};
+    std::atomic<uint64_t> killed{0};
+    std::thread killer([&] {
+        std::mt19937 rng(7);
+        while (!stop.load()) {
+            Conn* victim;
+            {
+                std::lock_guard<std::mutex> g(table_lock);
+                const size_t i = rng() % table.size();
+                victim = table[i];
+                table[i] = new Conn;
+            }
+            batch.Forget(*victim);   // returns once no flush will touch it
+            delete victim;
+            ++killed;
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+    });
+    const std::vector<uint8_t> f = unmasked_frame(40, 0x5A);
+    size_t delivered = 0;
+    for (int round = 0; round < 400; ++round) {
+        {
+            std::lock_guard<std::mutex> g(table_lock);
+            for (Conn* c : table)
+                for (int k = 0; k < 3; ++k)
+                    batch.Feed(*c, f.data(), f.size());
+        }
+        delivered += batch.Flush();
+    }
+    stop = true;
+    killer.join();
+    CHECK(delivered > 0);
+    CHECK(killed.load() > 0);
+    std::lock_guard<std::mutex> g(table_lock);
+    for (Conn* c : table)
+        delete c;
+}
+
+// The same for a send batch: transports are forgotten and deleted while
+// another thread's flush hands frames out.
+static void test_send_forget_while_flushing()
+{
+    WSSendBatch batch(nullptr);
+    std::mutex table_lock;
+    std::vector<Sink*> table;
+    for (int i = 0; i < 12; ++i)
+        table.push_back(new Sink);
+    std::atomic<bool> stop{false};
+    std::atomic<uint64_t> killed{0};
+    std::thread killer([&] {
+        std::mt19937 rng(11);
+        while (!stop.load()) {
+            Sink* victim;
+            {
+                std::lock_guard<std::mutex> g(table_lock);
+                const size_t i = rng() % table.size();
+                victim = table[i];
+                table[i] = new Sink;
+            }
+            batch.Forget(*victim);
+            delete victim;
+            ++killed;
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+    });
+    const uint8_t payload[32] = {1, 2, 3};
+    size_t sent = 0;
+    for (int round = 0; round < 400; ++round) {
+        {
+            std::lock_guard<std::mutex> g(table_lock);
+            for (Sink* t : table)
+                for (int k = 0; k < 3; ++k)
+                    batch.Queue(*t, 0, 0x82, false, payload, sizeof payload);
+        }
+        sent += batch.Flush();
+    }
+    stop = true;
+    killer.join();
+    CHECK(sent > 0);
+    CHECK(killed.load() > 0);
+    std::lock_guard<std::mutex> g(table_lock);
+    for (Sink* t : table)
+        delete t;
+}
+
+// Frames a session queued into ANOTHER thread's BatchScope (a SendAsync
+// from a worker): destroying the session on this thread drops them from that
+// thread's batch (BatchScope::ForgetEverywhere), so the scope's end does not
+// hand a frame to the destroyed transport.
+static void test_session_destroyed_while_queued_elsewhere()
+{
+    constexpr int n = 6, victim = 2;
+    std::vector<Sink*> sinks;
+    std::vector<WSSession*> sessions;
+    for (int i = 0; i < n; ++i) {
+        sinks.push_back(new Sink);
+        sessions.push_back(new WSSession(*sinks.back()));
+    }
+    std::mutex m;
+    std::condition_variable cv;
+    int phase = 0;
+    std::thread worker([&] {
+        BatchScope scope;   // e.g. an event-loop tick on a worker thread
+        for (WSSession* s : sessions)
+            CHECK(s->SendBinaryAsync("hello"));
+        std::unique_lock<std::mutex> g(m);
+        phase = 1;
+        cv.notify_all();
+        cv.wait(g, [&] { return phase == 2; });
+        // the scope ends here: its flush hands out what is still queued
+    });
+    {
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] { return phase == 1; });
+    }
+    delete sessions[victim];   // ~WSSession: ForgetEverywhere
+    delete sinks[victim];
+    sessions[victim] = nullptr;
+    sinks[victim] = nullptr;
+    {
+        std::lock_guard<std::mutex> g(m);
+        phase = 2;
+    }
+    cv.notify_all();
+    worker.join();
+    for (int i = 0; i < n; ++i) {
+        if (i == victim)
+            continue;
+        CHECK(sinks[i]->frames.load() == 1);
+        CHECK(sinks[i]->bytes.load() == 2 + 5);   // 82 05 "hello"
+        delete sessions[i];
+        delete sinks[i];
+    }
+}
+
+int main()
+{
+    test_receive_forget_while_flushing();
+    test_send_forget_while_flushing();
+    test_session_destroyed_while_queued_elsewhere();
+    std::printf("%d checks, %d failures\n", g_checks.load(), g_failures.load());
+    return g_failures.load() == 0 ? 0 : 1;
+}

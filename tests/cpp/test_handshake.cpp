@@ -5,6 +5,7 @@
 // upgrade over an in-memory transport.
 #include "server/http/http_request.h"
 #include "server/http/http_response.h"
+#include "server/ws/ws_batch.h"
 #include "server/ws/ws_client.h"
 #include "server/ws/ws_handshake.h"
 #include "server/ws/ws_session.h"
@@ -15,13 +16,36 @@
 #include "tls_test_certs.h"
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <deque>
+#include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
 using namespace CppServer;
 using namespace CppServer::WS;
+
+#ifdef WSG_TEST_HEAP_PINNED
+// CPU-suite build (no device): the batches' page-locked buffers come from
+// wsg_host_alloc (HIP); these definitions take the place of libwsg.so's
+// (symbol interposition) with heap memory, which is all a batch needs when
+// no GPU pass runs (key-0 frames).
+extern "C" int wsg_host_alloc(size_t bytes, void** out)
+{
+    *out = std::malloc(bytes ? bytes : 1);
+    return *out ? WSG_OK : WSG_ENOMEM;
+}
+extern "C" int wsg_host_free(void* p)
+{
+    std::free(p);
+    return WSG_OK;
+}
+#endif
 
 static int g_failures = 0, g_checks = 0;
 #define CHECK(cond)                                                                    \
@@ -241,6 +265,7 @@ struct MyWssClient : WSSClient {
     }
     void onWSConnected(const HTTP::HTTPResponse&) override { up = true; }
     void onWSError(const std::string& message) override { err = message; }
+    void use_send_key(uint32_t key) { set_send_key(key); }
     void onHandshaked() override
     {
         tls_up = true;
@@ -396,6 +421,113 @@ static void test_wss_upgrade()
     }
 }
 
+// a WSS client that queues a request with SendTextAsync inside a
+// BatchScope and then waits in a synchronous ReceiveText: the TLS layer held
+// the request's records until the scope ends, and the receive waited for a
+// reply to bytes never sent.  The server runs on its own thread here (a
+// socket peer); records travel through locked inboxes.
+struct ThreadLoop : Transport {
+    ThreadLoop* peer = nullptr;
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<uint8_t> inbox;
+    size_t Send(const void* b, size_t n) override
+    {
+        const uint8_t* p = static_cast<const uint8_t*>(b);
+        {
+            std::lock_guard<std::mutex> g(peer->m);
+            peer->inbox.insert(peer->inbox.end(), p, p + n);
+        }
+        peer->cv.notify_all();
+        return n;
+    }
+    bool SendAsync(const void* b, size_t n) override { return Send(b, n) == n; }
+    // what arrived within 2 s (0: nothing came)
+    size_t Receive(void* buf, size_t n) override
+    {
+        std::unique_lock<std::mutex> g(m);
+        cv.wait_for(g, std::chrono::seconds(2), [&] { return !inbox.empty(); });
+        const size_t k = std::min(n, inbox.size());
+        std::copy_n(inbox.begin(), k, static_cast<uint8_t*>(buf));
+        inbox.erase(inbox.begin(), inbox.begin() + std::ptrdiff_t(k));
+        return k;
+    }
+    std::vector<uint8_t> take()
+    {
+        std::lock_guard<std::mutex> g(m);
+        std::vector<uint8_t> v(inbox.begin(), inbox.end());
+        inbox.clear();
+        return v;
+    }
+    bool Disconnect() override { return true; }
+    bool IsConnected() const override { return true; }
+};
+
+struct EchoWssSession : MyWssSession {
+    using MyWssSession::MyWssSession;
+    void onWSReceived(const void* buffer, size_t size) override { SendTextAsync(buffer, size); }
+};
+
+static void test_wss_sync_receive_in_scope()
+{
+    using CppServer::Asio::SSLContext;
+    const TestPki pki = make_test_pki();
+    auto server_ctx = std::make_shared<SSLContext>(asio::ssl::context::tlsv13);
+    server_ctx->use_certificate_chain(pki.server_cert_pem.data(), pki.server_cert_pem.size());
+    server_ctx->use_private_key(pki.server_key_pem.data(), pki.server_key_pem.size(), asio::ssl::context::pem);
+    auto client_ctx = std::make_shared<SSLContext>(asio::ssl::context::tlsv13);
+    client_ctx->set_verify_mode(asio::ssl::verify_peer | asio::ssl::verify_fail_if_no_peer_cert);
+    client_ctx->add_certificate_authority(pki.ca_pem.data(), pki.ca_pem.size());
+
+    ThreadLoop a, b;
+    a.peer = &b;
+    b.peer = &a;
+    MyWssClient client(client_ctx, a);
+    EchoWssSession session(server_ctx, b);
+    CHECK(session.Connect());
+    CHECK(client.Connect());
+    // the TLS handshake and the upgrade, pumped on this thread
+    for (int guard = 0; guard < 64 && !(client.up && session.up); ++guard) {
+        const std::vector<uint8_t> rb = b.take(), ra = a.take();
+        if (!rb.empty())
+            session.onReceived(rb.data(), rb.size());
+        if (!ra.empty())
+            client.onReceived(ra.data(), ra.size());
+    }
+    CHECK(client.up && session.up);
+    // key 0 on the client: the frames stay masked-format, with nothing to
+    // XOR, so no GPU pass runs on either side (this is the CPU suite)
+    client.use_send_key(0);
+    std::atomic<bool> stop{false};
+    std::thread server([&] {
+        while (!stop.load()) {
+            std::vector<uint8_t> rec;
+            {
+                std::unique_lock<std::mutex> g(b.m);
+                b.cv.wait_for(g, std::chrono::milliseconds(20), [&] { return !b.inbox.empty(); });
+                rec.assign(b.inbox.begin(), b.inbox.end());
+                b.inbox.clear();
+            }
+            if (!rec.empty())
+                session.onReceived(rec.data(), rec.size());
+        }
+    });
+    std::string got, error;
+    try {
+        BatchScope scope;   // an event-loop tick on the client's thread
+        CHECK(client.SendTextAsync("ping"));
+        got = client.ReceiveText();
+    } catch (const std::exception& e) {
+        error = e.what();
+    }
+    stop = true;
+    server.join();
+    if (!error.empty())
+        std::fprintf(stderr, "test_wss_sync_receive_in_scope: %s\n", error.c_str());
+    CHECK(error.empty());
+    CHECK(got == "ping");
+}
+
 int main()
 {
     try {
@@ -405,6 +537,7 @@ int main()
         test_client_rules();
         test_client_session_upgrade();
         test_wss_upgrade();
+        test_wss_sync_receive_in_scope();
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());
         return 2;

@@ -8,9 +8,12 @@ of a node, framed output gathered to one rank) on the GPU.
 * the multi-process flow at world size 2 (gloo, both ranks on cuda:0): each
   rank encodes its shard with the HIP kernels, the shards are gathered and
   reassembled, and the job equals the oracle's encode of the whole job;
-* the C-ABI multi-GPU entry (wsg_mgpu_encode_gather over RCCL) at world size
-  1 — the only RCCL group one GPU allows — in both of its forms (one process
-  driving its devices; one rank per process), against the oracle.
+* the C-ABI multi-GPU entry (wsg_mgpu_encode_gather): the one-process form
+  at world sizes 1, 2, 3 and 8 with every rank on the one GPU (device
+  copies to the root), chunk sizes 1, 300, 700 and 1024, ragged jobs, other
+  roots, ranks holding nothing, an encode error on a non-root rank; the
+  RCCL rank-per-process form at world size 1, the only RCCL group one GPU
+  allows; all against the oracle.
 """
 import os
 import socket
@@ -185,6 +188,99 @@ def test_mgpu_rejects_wrong_shard():
         with pytest.raises(ca.WSGError) as e:
             g.encode_gather(100, 10, [p], [d], [w], [o], out=w.clone())
         assert e.value.code == ca.WSG_EINVAL
+    finally:
+        g.close()
+
+
+def _world_job(world, n, chunk, seed, root=0, bad_rank=None):
+    """The one-process group at `world` ranks, all on device 0: the job's
+    round-robin shards encoded per rank, gathered to `root` by device
+    copies; the root's wire and offsets against the oracle's encode of the
+    whole job.  bad_rank: that rank's wire buffer is too short (its encode
+    latches WSG_ENOMEM), which must stop the call on every rank."""
+    payload, desc = _ragged_job(n, seed)
+    ref, ref_off = oracle.encode_batch(payload, desc)
+    g = ca.MultiGPU([0] * world)
+    assert (g.world, g.nlocal, g.first_rank) == (world, world, 0)
+    try:
+        p = torch.from_numpy(payload).cuda()   # every rank's descriptors point into the one arena
+        descs, wires, woffs = [], [], []
+        for r in range(world):
+            ids = shard.rank_frames(r, world, n, chunk)
+            assert len(ids) == ca.MultiGPU.shard_count(n, chunk, world, r)
+            d = desc[ids]
+            cap = int(ca.frame_sizes(d).sum()) if len(ids) else 0
+            if r == bad_rank:
+                cap //= 2
+            descs.append(ca.desc_to_tensor(d, "cuda") if len(ids) else torch.empty(0, dtype=torch.uint8,
+                                                                                   device="cuda"))
+            wires.append(torch.empty(max(cap, 16), dtype=torch.uint8, device="cuda"))
+            woffs.append(torch.empty(len(ids) + 1, dtype=torch.int64, device="cuda"))
+        out = torch.full((len(ref) + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+        out_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        if bad_rank is not None:
+            with pytest.raises(ca.WSGError) as e:
+                g.encode_gather(n, chunk, [p] * world, descs, wires, woffs, root=root, out=out, out_off=out_off)
+            assert e.value.code == ca.WSG_ENOMEM
+            return
+        enc_ms, gat_ms = g.encode_gather(n, chunk, [p] * world, descs, wires, woffs, root=root, out=out,
+                                         out_off=out_off)
+        got = out.cpu().numpy()
+        assert np.array_equal(got[: len(ref)], ref)
+        assert (got[len(ref):] == 0xA5).all()
+        assert np.array_equal(out_off.cpu().numpy().view(np.uint64), ref_off)
+        assert enc_ms >= 0 and gat_ms >= 0
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("n,chunk", [(1000, 1), (5000, 700), (9000, 1024)])
+def test_mgpu_world_n_one_device(world, n, chunk):
+    """the world > 1 placement (chunk sizes, chunk offsets
+    in job order, per-chunk transfers, rank-by-rank offset stage, rebase) run
+    with every rank on the one GPU."""
+    _world_job(world, n, chunk, seed=world * 7919 + n + chunk)
+
+
+@pytest.mark.parametrize("world,root", [(3, 2), (8, 5)])
+def test_mgpu_world_n_other_root(world, root):
+    _world_job(world, 4000, 300, seed=11 + world, root=root)
+
+
+def test_mgpu_world_fewer_chunks_than_ranks():
+    """8 ranks, 3 chunks: five ranks hold nothing."""
+    _world_job(8, 2500, 1024, seed=5)
+
+
+@pytest.mark.parametrize("bad_rank", [1, 2])
+def test_mgpu_error_on_non_root_rank(bad_rank):
+    """An encode error on a non-root rank stops the whole call (status round)."""
+    _world_job(3, 3000, 500, seed=17, root=0, bad_rank=bad_rank)
+
+
+def test_mgpu_world8_c5_shape_one_device():
+    """C5-shape frames (16 KiB payloads) at world 8 on one device, 64 Ki frames."""
+    n, chunk = 1 << 16, 1024
+    g = ca.MultiGPU([0] * 8)
+    try:
+        ids_all = np.arange(n)
+        ref_off = np.arange(n + 1, dtype=np.uint64) * np.uint64(FSZ)
+        payloads, descs, wires, woffs = [], [], [], []
+        for r in range(8):
+            ids = shard.rank_frames(r, 8, n, chunk)
+            payloads.append(wl.c5_payload_torch(ids, SIZE, device="cuda"))
+            descs.append(ca.desc_to_tensor(wl.c5_desc(ids, SIZE), "cuda"))
+            wires.append(torch.empty(len(ids) * FSZ, dtype=torch.uint8, device="cuda"))
+            woffs.append(torch.empty(len(ids) + 1, dtype=torch.int64, device="cuda"))
+        out = torch.empty(n * FSZ, dtype=torch.uint8, device="cuda")
+        out_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        g.encode_gather(n, chunk, payloads, descs, wires, woffs, root=0, out=out, out_off=out_off)
+        assert np.array_equal(out_off.cpu().numpy().view(np.uint64), ref_off)
+        keys = torch.from_numpy(wl.c5_desc(ids_all, SIZE)["key"].view(np.int32).copy()).cuda()
+        words = out.view(torch.int32).view(n, FSZ // 4)
+        exp = _expected_words(torch.from_numpy(ids_all).cuda(), keys)
+        assert torch.equal(words, exp)
     finally:
         g.close()
 

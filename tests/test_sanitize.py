@@ -7,6 +7,9 @@ drop-in compile check (CPU only, no GPU).
   round trips, split streams, garbage streams and frame tables, mutated HTTP
   requests), and the handshake test with the product's host sources
   (ws.cpp, ws_api.cpp, ws_batch.cpp, http.cpp) instrumented;
+* `make -C tests/cpp threads` builds the batches' cross-thread test
+  (tests/cpp/test_batch_threads.cpp) with the product's host sources under
+  ThreadSanitizer and under AddressSanitizer;
 * `make -C tests/cpp dropin` compiles code written against the reference's
   WebSocket API signatures (Timespan overloads, PerformClientUpgrade(response,
   UUID), ConnectAsync) against include/server/ws/.
@@ -41,6 +44,24 @@ def test_sanitized_oracle_and_http():
 def test_sanitized_handshake():
     _make("sanitize")
     _run(os.path.join(CPP, "_build", "san", "test_handshake"))
+
+
+def test_batch_threads_tsan():
+    """Forget / destroy a connection or transport on one thread
+    while another flushes, and destroy a session whose frames sit in another
+    thread's BatchScope (tests/cpp/test_batch_threads.cpp, ThreadSanitizer)."""
+    _make("threads")
+    exe = os.path.join(CPP, "_build", "san", "test_batch_threads_tsan")
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "0 failures" in r.stdout
+    assert "WARNING: ThreadSanitizer" not in r.stderr
+
+
+def test_batch_threads_asan():
+    _make("threads")
+    _run(os.path.join(CPP, "_build", "san", "test_batch_threads_asan"))
 
 
 def test_reference_api_compiles():

@@ -340,6 +340,21 @@ __global__ __launch_bounds__(256) void k_policy(const uint8_t* __restrict__ src,
 // consecutive 1 KiB rows (RW * 64 lanes... one 16-B chunk per lane per row)
 // per pass, passes strided by the whole grid; SC1 = write-through stores.
 // an (almost) empty kernel: the launch / wave start-up floor of a grid
+// random source bytes (a 32-bit hash of the word index): the data the codec
+// streams, against hipMemset's constant bytes
+__global__ __launch_bounds__(256) void k_hashfill(uint32_t* __restrict__ dst, uint64_t words, uint32_t seed)
+{
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < words; i += uint64_t(gridDim.x) * 256) {
+        uint32_t x = uint32_t(i) ^ uint32_t(i >> 32) * 0x9E3779B1u ^ seed;
+        x ^= x >> 16;
+        x *= 0x7FEB352Du;
+        x ^= x >> 15;
+        x *= 0x846CA68Bu;
+        x ^= x >> 16;
+        dst[i] = x;
+    }
+}
+
 __global__ void k_empty(uint32_t* out, uint32_t v)
 {
     if (v == 0xFFFFFFFFu)
@@ -935,6 +950,64 @@ int main(int argc, char** argv)
             }
         CK(hipFree(s2));
         CK(hipFree(d2));
+        CK(hipFree(src));
+        CK(hipFree(dst));
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "power") {
+        // C5's question, second part: per-launch times of a long back-to-back
+        // run of the covering wave-piece copy on constant (hipMemset) vs
+        // random source bytes; argv[3] launches (default 40)
+        const int launches = argc > 3 ? atoi(argv[3]) : 40;
+        const uint64_t pieces = n16 / 256;
+        const int grid = int(pieces / 4);
+        for (int random = 0; random < 2; ++random) {
+            if (random)
+                k_hashfill<<<cus * 64, 256>>>((uint32_t*)src, bytes / 4, 12345u);
+            else
+                CK(hipMemset(src, 1, bytes));
+            CK(hipDeviceSynchronize());
+            std::vector<hipEvent_t> ev(launches + 1);
+            for (int i = 0; i <= launches; ++i)
+                CK(hipEventCreate(&ev[i]));
+            CK(hipEventRecord(ev[0]));
+            for (int i = 0; i < launches; ++i) {
+                k_wavepiece<256, 4, 3><<<grid, 256>>>(src, dst, n16, 0x12345678u);
+                CK(hipEventRecord(ev[i + 1]));
+            }
+            CK(hipEventSynchronize(ev[launches]));
+            printf("%s source, %d launches (us):", random ? "random" : "constant", launches);
+            double first = 0, last = 0;
+            for (int i = 0; i < launches; ++i) {
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+                printf(" %.0f", ms * 1e3);
+                if (i < 5)
+                    first += ms / 5;
+                if (i >= launches - 5)
+                    last += ms / 5;
+            }
+            printf("\n  first 5 avg %.1f us = %.1f GB/s, last 5 avg %.1f us = %.1f GB/s\n", first * 1e3,
+                   2.0 * bytes / (first * 1e-3) / 1e9, last * 1e3, 2.0 * bytes / (last * 1e-3) / 1e9);
+            for (int i = 0; i <= launches; ++i)
+                CK(hipEventDestroy(ev[i]));
+        }
+        CK(hipFree(src));
+        CK(hipFree(dst));
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "footprint") {
+        // C5's footprint question (round 3): the encode pattern (one 4 KiB
+        // piece per wave) with a grid capped at 1024 blocks/CU — pieces dealt
+        // grid-stride, so once the buffer has more pieces than the grid has
+        // waves the resident waves work several regions GiB apart — against a
+        // grid that covers every piece once (one pass, dispatch order = address
+        // order), and the resident grid-stride copy (32 blocks/CU)
+        for (int rep = 0; rep < 2; ++rep) {
+            run_wp<256, 4>("wavepiece capped", src, dst, n16, cus, 1024);
+            run_wp<256, 4>("wavepiece covering", src, dst, n16, cus, 1 << 22);
+            run<256, 4, 3>("resident grid-stride", src, dst, n16, cus, 32);
+        }
         CK(hipFree(src));
         CK(hipFree(dst));
         return 0;
