@@ -910,6 +910,38 @@ def roofline_obj(kernel, alg_bytes, avg_ms, traffic, timing):
             "avg_kernel_ms": round(avg_ms, 5), "kernel_timing": timing}
 
 
+_ROCTX = []
+
+
+def marker(name):
+    """A roctx range around a leg's timed region (rocprofv3 --marker-trace
+    lines the kernels of a trace up with the bench objects:
+    tools/trace_split.py); a no-op where the roctx library is absent."""
+    import contextlib
+    import ctypes
+
+    if not _ROCTX:
+        try:
+            lib = ctypes.CDLL("librocprofiler-sdk-roctx.so.1")
+            lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+            _ROCTX.append(lib)
+        except OSError:
+            _ROCTX.append(None)
+
+    @contextlib.contextmanager
+    def rng():
+        lib = _ROCTX[0]
+        if lib is not None:
+            lib.roctxRangePushA(name.encode())
+        try:
+            yield
+        finally:
+            if lib is not None:
+                lib.roctxRangePop()
+
+    return rng()
+
+
 def timed_region(w, steps, world, device):
     """EXACTLY `steps` steps between barrier + torch.cuda.synchronize() on
     both sides (wall clock, max over ranks), with the dominant kernels' HIP
@@ -935,12 +967,13 @@ def timed_region(w, steps, world, device):
     e1.record()
     barrier(world)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e0.record()
-    for _ in range(steps):
-        w.step()
-    e1.record()
-    torch.cuda.synchronize()
+    with marker("bench.%s.timed" % w.cfg):
+        t0 = time.perf_counter()
+        e0.record()
+        for _ in range(steps):
+            w.step()
+        e1.record()
+        torch.cuda.synchronize()
     barrier(world)
     elapsed = time.perf_counter() - t0
     region_ms = e0.elapsed_time(e1)
@@ -1003,7 +1036,7 @@ def config_obj(args, cfg, codec, rank, world, device, steps, warmup, cpu):
         w.close()
 
 
-def decode_launches(w, launches=30):
+def decode_launches(w, launches=60):
     """C3's decode half launch by launch: k_decode alone
     on the round trip's wire, HIP events between launches (one launch per
     decode_batch call), after the timed region (the GPU is warm)."""
@@ -1021,8 +1054,13 @@ def decode_launches(w, launches=30):
     t.cuda.synchronize()
     ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(launches)]
     med = statistics.median(ms)
+    srt = sorted(ms)
+    p10, p90 = srt[launches // 10], srt[(9 * launches) // 10]
     return {"launches": launches, "median_ms": round(med, 5), "min_ms": round(min(ms), 5),
-            "max_ms": round(max(ms), 5), "spread_pct": round(100 * (max(ms) - min(ms)) / med, 2),
+            "max_ms": round(max(ms), 5), "p10_ms": round(p10, 5), "p90_ms": round(p90, 5),
+            "stdev_ms": round(statistics.pstdev(ms), 5), "spread_pct": round(100 * (max(ms) - min(ms)) / med, 2),
+            "p10_p90_spread_pct": round(100 * (p90 - p10) / med, 2),
+            "first_5_ms": [round(x, 4) for x in ms[:5]],
             "frac_at_median": round(w.dec_alg_bytes / (med * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
 
 

@@ -15,6 +15,8 @@ $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws.cpp -o w.
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws_api.cpp -o a.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws_batch.cpp -o b.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/http.cpp -o h.o
+$H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/tls.cpp -o t.o
+$H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/wss.cpp -o s.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/wsg_mgpu.cpp -o m.o
-$H --offload-arch=gfx950 -shared -o libwsg.so k.o c.o w.o a.o b.o h.o m.o -lcrypto -ldl -L/opt/rocm/lib -lrocprofiler-sdk-roctx
+$H --offload-arch=gfx950 -shared -o libwsg.so k.o c.o w.o a.o b.o h.o t.o s.o m.o -lssl -lcrypto -ldl -L/opt/rocm/lib -lrocprofiler-sdk-roctx
 echo "$out/libwsg.so"
