@@ -900,14 +900,19 @@ def fanout_many_leg(w, m=16, reps=10):
             "write_GBps": round(bytes_out / (ms * 1e-3) / 1e9, 1), "frame_bytes": fsz}
 
 
-def roofline_obj(kernel, alg_bytes, avg_ms, traffic, timing):
+def roofline_obj(kernel, alg_bytes, avg_ms, traffic, timing, minmax=None):
     """The roofline object of one kernel: algorithmic bytes per launch over
     its average launch duration (HIP events on its launch stream), against
-    the HBM peak; `traffic` = PMC HBM bytes per launch (profiles/), or None."""
+    the HBM peak; `traffic` = PMC HBM bytes per launch (profiles/), or None;
+    `minmax` = (shortest, longest) timed launch, where each launch is timed."""
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms else 0.0
-    return {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
-            "avg_kernel_ms": round(avg_ms, 5), "kernel_timing": timing}
+    r = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
+         "avg_kernel_ms": round(avg_ms, 5), "kernel_timing": timing}
+    if minmax is not None and avg_ms:
+        r.update({"launch_min_ms": round(minmax[0], 5), "launch_max_ms": round(minmax[1], 5),
+                  "launch_spread_pct": round(100 * (minmax[1] - minmax[0]) / avg_ms, 2)})
+    return r
 
 
 _ROCTX = []
@@ -978,11 +983,12 @@ def timed_region(w, steps, world, device):
     elapsed = time.perf_counter() - t0
     region_ms = e0.elapsed_time(e1)
     if single:
-        kern = [(region_ms, steps)]
+        kern, spread = [(region_ms, steps)], [None]
         note = "HIP events around the timed region / steps (one launch per step)"
     else:
-        kern = []
+        kern, spread = [], []
         for c in codecs:
+            spread.append(c.timing_minmax())
             kern.append(c.timing_read(reset=True))
             c.timing(False)
         note = ("HIP events around the dominant kernel of every call in the timed region" if every == 1 else
@@ -990,7 +996,8 @@ def timed_region(w, steps, world, device):
     w.codec.sync()
     elapsed = max_over_ranks(elapsed, world, device)
     avgs = [max_over_ranks(ms / max(k, 1), world, device) for ms, k in kern]
-    return {"elapsed": elapsed, "region_event_ms": region_ms, "kernel_avg_ms": avgs, "timing": note}
+    return {"elapsed": elapsed, "region_event_ms": region_ms, "kernel_avg_ms": avgs, "timing": note,
+            "minmax": spread}
 
 
 def config_obj(args, cfg, codec, rank, world, device, steps, warmup, cpu):
@@ -1014,10 +1021,11 @@ def config_obj(args, cfg, codec, rank, world, device, steps, warmup, cpu):
                "unit": "GiB/s", "steps": steps, "warmup": warmup, "ms_per_step": round(ms_step, 4),
                "event_ms_per_step": round(r["region_event_ms"] / steps, 4)}
         obj.update(w.extra)
-        rf = roofline_obj(w.kernel, w.alg_bytes, r["kernel_avg_ms"][0], pmc_traffic(args.pmc, cfg), r["timing"])
+        rf = roofline_obj(w.kernel, w.alg_bytes, r["kernel_avg_ms"][0], pmc_traffic(args.pmc, cfg), r["timing"],
+                          r["minmax"][0])
         if cfg == "c3":
             dec = roofline_obj("k_decode", w.dec_alg_bytes, r["kernel_avg_ms"][1], pmc_traffic(args.pmc, "c3_dec"),
-                               r["timing"])
+                               r["timing"], r["minmax"][1])
             both = w.alg_bytes + w.dec_alg_bytes
             t = sum(r["kernel_avg_ms"])
             rf = dict(dec, halves=[rf, dec],
@@ -1111,10 +1119,11 @@ def main():
     k_avg_ms = r["kernel_avg_ms"][0]
     pmc_key = w.cfg + ("x%d" % w.m if w.cfg == "c4" and w.m > 1 else "")
     traffic = pmc_traffic(args.pmc, pmc_key) if args.frames is None and args.size is None else None
-    roof = roofline_obj(w.kernel, w.alg_bytes, k_avg_ms, traffic, r["timing"])
+    roof = roofline_obj(w.kernel, w.alg_bytes, k_avg_ms, traffic, r["timing"], r["minmax"][0])
     if w.cfg == "c3":
         dec = roofline_obj("k_decode", w.dec_alg_bytes, r["kernel_avg_ms"][1],
-                           pmc_traffic(args.pmc, "c3_dec") if traffic is not None else None, r["timing"])
+                           pmc_traffic(args.pmc, "c3_dec") if traffic is not None else None, r["timing"],
+                           r["minmax"][1])
         roof = dict(dec, halves=[roof, dec])
 
     extras = {"event_ms_per_step": round(r["region_event_ms"] / args.steps, 4)}

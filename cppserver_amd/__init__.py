@@ -106,6 +106,7 @@ def lib(path=None):
         "wsg_mgpu_encode_batch_host": (ci, [vp, vp, u64, vp, u32, vp, u64, vp]),
         "wsg_timing_enable": (ci, [vp, ci]),
         "wsg_timing_read": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ci]),
+        "wsg_timing_minmax": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
         if path is not None and not hasattr(L, name):
@@ -360,6 +361,12 @@ class Codec:
     def timing(self, on=True, every=1):
         """Time the dominant kernel of every `every`-th batch call (HIP events)."""
         _check(self._L.wsg_timing_enable(self._ctx, int(every) if on else 0), "wsg_timing_enable")
+
+    def timing_minmax(self):
+        """(shortest, longest) timed launch in ms since the last reset."""
+        lo, hi = ctypes.c_double(), ctypes.c_double()
+        _check(self._L.wsg_timing_minmax(self._ctx, ctypes.byref(lo), ctypes.byref(hi)), "wsg_timing_minmax")
+        return lo.value, hi.value
 
     def timing_read(self, reset=True):
         ms, n = ctypes.c_double(), ctypes.c_uint64()

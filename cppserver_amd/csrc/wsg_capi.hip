@@ -101,6 +101,7 @@ struct wsg_ctx {
     std::vector<EvPair> pending, pool;
     double acc_ms = 0.0;
     uint64_t launches = 0;
+    double min_ms = 0.0, max_ms = 0.0;   // extremes of the launches since the last reset
 };
 
 namespace {
@@ -217,6 +218,8 @@ int drain_timing(wsg_ctx* c)
         float ms = 0.f;
         WSG_HIP(hipEventElapsedTime(&ms, ev.a, ev.b));
         c->acc_ms += ms;
+        c->min_ms = c->launches ? std::min(c->min_ms, double(ms)) : double(ms);
+        c->max_ms = c->launches ? std::max(c->max_ms, double(ms)) : double(ms);
         c->launches += 1;
         c->pool.push_back(ev);
     }
@@ -1172,7 +1175,21 @@ int wsg_timing_read(wsg_ctx* c, double* total_ms, uint64_t* launches, int reset)
     if (reset) {
         c->acc_ms = 0.0;
         c->launches = 0;
+        c->min_ms = c->max_ms = 0.0;
     }
+    return WSG_OK;
+}
+
+int wsg_timing_minmax(wsg_ctx* c, double* min_ms, double* max_ms)
+{
+    if (!c)
+        return WSG_EINVAL;
+    if (int rc = drain_timing(c))
+        return rc;
+    if (min_ms)
+        *min_ms = c->min_ms;
+    if (max_ms)
+        *max_ms = c->max_ms;
     return WSG_OK;
 }
 

@@ -330,6 +330,9 @@ int wsg_timing_enable(wsg_ctx* ctx, int on);
 /* Sum of the dominant-kernel durations (ms) and launch count since the last
  * reset; synchronizes outstanding events.                                     */
 int wsg_timing_read(wsg_ctx* ctx, double* total_ms, uint64_t* launches, int reset);
+/* Shortest and longest of those durations (ms) since the last reset (0, 0
+ * when none); synchronizes outstanding events, resets nothing.              */
+int wsg_timing_minmax(wsg_ctx* ctx, double* min_ms, double* max_ms);
 
 #ifdef __cplusplus
 }
