@@ -25,8 +25,12 @@ run() {   # name, timeout, command...
 }
 if [ "${BENCH:-1}" = 1 ]; then
     run bench 600 python bench.py --steps 20 --warmup 5
-    run trace 900 rocprofv3 --kernel-trace --marker-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
-        python bench.py --steps 20 --warmup 5
+    # the same command; its host-side child legs (echo, multicast, session
+    # batches: no kernel of the GPU legs) are skipped, tracing them takes minutes
+    export WSG_BENCH_HOST_LEGS=0
+    run trace 900 rocprofv3 --kernel-trace --marker-trace --stats -d "$OUT/trace" -o run \
+        --output-format csv -- python bench.py --steps 20 --warmup 5
+    unset WSG_BENCH_HOST_LEGS
 fi
 [ "${PMC:-1}" = 1 ] && for c in ${CFGS:-c2 c3 c4 c5}; do
     for k in FETCH_SIZE WRITE_SIZE; do
