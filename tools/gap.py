@@ -19,7 +19,22 @@ import cppserver_amd as ca  # noqa: E402
 from cppserver_amd import workloads as wl  # noqa: E402
 
 
+def spin_sync():
+    """$WSG_SPIN=1: hipDeviceScheduleSpin on the HIP runtime torch loaded,
+    before the device is initialised (the host spins in synchronize instead
+    of yielding / sleeping)."""
+    import ctypes
+    import glob
+
+    libs = glob.glob(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so*"))
+    hip = ctypes.CDLL(libs[0] if libs else "libamdhip64.so")
+    rc = hip.hipSetDeviceFlags(ctypes.c_uint(1))   # hipDeviceScheduleSpin
+    print("hipSetDeviceFlags(spin) ->", rc, libs[:1], flush=True)
+
+
 def main():
+    if os.environ.get("WSG_SPIN") == "1":
+        spin_sync()
     n, size = 4096, 65536
     wire, fs, _ = wl.c2_wire(n, size, seed=1)
     ws = [torch.from_numpy(wire).cuda(), torch.from_numpy(wl.c2_wire(n, size, seed=2)[0]).cuda()]
@@ -29,7 +44,9 @@ def main():
     c = ca.Codec(0)
     launch = [c.prepare_decode(ws[i], f, outs[i], info) for i in range(2)]
 
-    def region(k, poll):
+    def region(k, poll, pause=0.0):
+        if pause:
+            time.sleep(pause)   # bench.py's spot check leaves the GPU idle for seconds
         for i in range(5):
             launch[i & 1]()
         c.sync()
@@ -57,6 +74,11 @@ def main():
             print("poll=%d K=%3d  wall %9.1f us  events %9.1f us  gap %7.1f us  (%.2f us/step)  submit %8.1f us"
                   % (poll, k, wall, ev, wall - ev, (wall - ev) / max(k, 1), sub), flush=True)
 
+    # as bench.py meets it: a pause, 5 warm-up steps, 20 timed
+    rows = [region(20, False, pause=1.5) for _ in range(5)]
+    for wall, ev, sub in rows:
+        print("after 1.5 s idle: K= 20  wall %8.1f us  events %8.1f us  gap %6.1f us (%.2f%%)" % (
+            wall, ev, wall - ev, 100 * (wall - ev) / ev), flush=True)
     # per-launch events over a 20-launch region
     for trial in range(3):
         for i in range(5):
