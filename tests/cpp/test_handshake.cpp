@@ -31,7 +31,7 @@ using namespace CppServer;
 using namespace CppServer::WS;
 
 #ifdef WSG_TEST_HEAP_PINNED
-// CPU-suite build (no device): the batches' page-locked buffers come from
+// Host-only test (it runs in the CPU suite, no device): the batches' page-locked buffers come from
 // wsg_host_alloc (HIP); these definitions take the place of libwsg.so's
 // (symbol interposition) with heap memory, which is all a batch needs when
 // no GPU pass runs (key-0 frames).
