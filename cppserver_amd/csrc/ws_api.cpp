@@ -434,15 +434,20 @@ void WSServer::AddSession(const std::shared_ptr<WSSession>& session)
 
 void WSServer::RemoveSession(const std::shared_ptr<WSSession>& session)
 {
-    std::unique_lock<std::shared_mutex> locker(_sessions_lock);
-    if (std::find(_sessions.begin(), _sessions.end(), session) != _sessions.end()) {
-        if (_rx_batch)
-            session->SetReceiveBatch(nullptr);   // its queued frames are dropped with it
-        if (_tx_batch)
-            session->SetSendBatch(nullptr);
+    bool detach = false;
+    {
+        std::unique_lock<std::shared_mutex> locker(_sessions_lock);
+        detach = std::find(_sessions.begin(), _sessions.end(), session) != _sessions.end();
+        _sessions.erase(std::remove(_sessions.begin(), _sessions.end(), session), _sessions.end());
+        _snapshot = std::make_shared<const std::vector<std::shared_ptr<WSSession>>>(_sessions);
     }
-    _sessions.erase(std::remove(_sessions.begin(), _sessions.end(), session), _sessions.end());
-    _snapshot = std::make_shared<const std::vector<std::shared_ptr<WSSession>>>(_sessions);
+    // its queued frames are dropped with it; outside the sessions lock: the
+    // batches' Forget waits for a flush on another thread, whose callbacks
+    // may take that lock (a Multicast from onWSReceived)
+    if (detach) {
+        session->SetReceiveBatch(nullptr);
+        session->SetSendBatch(nullptr);
+    }
 }
 
 void WSServer::EnableBatchReceive(bool on)
@@ -458,9 +463,15 @@ void WSServer::EnableBatchReceive(bool on)
             s->SetReceiveBatch(_rx_batch.get());
         return;
     }
-    for (auto& s : _sessions)
+    // detach outside the sessions lock (see RemoveSession): each Forget
+    // waits for a flush in progress on another thread, so the batch is idle
+    // when it goes
+    std::unique_ptr<WSReceiveBatch> gone = std::move(_rx_batch);
+    const auto sessions = _sessions;
+    locker.unlock();
+    for (auto& s : sessions)
         s->SetReceiveBatch(nullptr);
-    _rx_batch.reset();
+    gone.reset();
 }
 
 void WSServer::SetBatchDevices(const std::vector<int>& devices)
@@ -488,9 +499,12 @@ void WSServer::EnableBatchSend(bool on)
             s->SetSendBatch(_tx_batch.get());
         return;
     }
-    for (auto& s : _sessions)
+    std::unique_ptr<WSSendBatch> gone = std::move(_tx_batch);
+    const auto sessions = _sessions;
+    locker.unlock();
+    for (auto& s : sessions)
         s->SetSendBatch(nullptr);
-    _tx_batch.reset();
+    gone.reset();
 }
 
 size_t WSServer::FlushSend() { return _tx_batch ? _tx_batch->Flush() : 0; }
