@@ -582,6 +582,25 @@ def echo_c1_leg(seconds=3.0, timeout=120):
         cr["what"] = ("reference codec algorithm (oracle restatement of ws.cpp:212-456, CPU) in this same in-memory "
                       "echo loop; compare with per_read_1c / per_read_100c_4t")
         out["cpu_reference"] = cr
+    # over real loopback TCP, the reference's own method (its drivers on
+    # 127.0.0.1): the drop-in classes and the reference algorithm on the CPU,
+    # same epoll loop (tools/_build/bench_echo_tcp; measurement-only sockets)
+    tcp = os.path.join(ROOT, "tools", "_build", "bench_echo_tcp")
+    if os.path.exists(tcp):
+        tr = {}
+        for leg, a in (("gpu_1c_1t", ["gpu", "1", "1"]), ("gpu_100c_4t", ["gpu", "100", "4"]),
+                       ("gpu_tick_100c_4t", ["gpu_tick", "100", "4"]),
+                       ("cpu_ref_1c_1t", ["cpu_ref", "1", "1"]), ("cpu_ref_100c_4t", ["cpu_ref", "100", "4"])):
+            r = _run_leg([tcp] + a + ["1000", "32", str(seconds)], timeout)
+            if r.returncode != 0:
+                tr[leg] = {"error": (r.stderr or r.stdout).strip()[-300:]}
+                continue
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            tr[leg] = {k: d[k] for k in ("msg_per_s", "MiB_per_s", "latency_ns", "total_messages", "payload_ok")}
+        tr["what"] = ("ws_echo over TCP 127.0.0.1 (one process, server and client on their own epoll threads): "
+                      "gpu = the drop-in WSClient/WSSession, cpu_ref = the oracle's restatement of the reference "
+                      "codec (no GPU); the published figures below are this method on an i7-4790K")
+        out["tcp_loopback"] = tr
     out["reference_published"] = {"msg_per_s_1c_1t": 160448, "msg_per_s_100c_4t": 594328,
                                   "wss_msg_per_s_1c_1t": 203343, "wss_msg_per_s_100c_4t": 818230,
                                   "hardware": "loopback sockets, i7-4790K (README.md:3312-3352, 3356-3396): "

@@ -36,13 +36,13 @@ def report(text, tag, kernel="_ZN3wsg8k_decode"):
 
 def cut(text, marker):
     assert marker in text, marker
-    return text.replace(marker, "continue;\n" + marker, 1)
+    return text.replace(marker, "return;\n" + marker, 1)   # inside process_tile
 
 
 if __name__ == "__main__":
     src = open(SRC).read()
-    staged = "        // staged: payload segments in LDS"
-    boundary = "            // boundary: per chunk"
+    staged = "    // staged: payload segments in LDS"
+    boundary = "        // boundary: per chunk"
     report(src, "full")
     report(cut(src, staged), "no-staged")
     report(cut(src, boundary), "no-boundary")
