@@ -35,6 +35,10 @@ struct wsg_ctx {
     int enc_blocks_per_cu = 32768;
     uint64_t enc_launch_pieces = 0;   // k_encode_mask: pieces per launch (0: all in one)
     uint64_t xor_direct_max = 64 << 10;   // per-call XOR: kernel on the pinned stage up to this size (A/B: $WSG_XOR_DIRECT_MAX)
+    // host batches up to this many wire bytes whose buffers are page-locked:
+    // the kernels read and write them in place (one launch sequence and one
+    // synchronize, no staging copies); $WSG_HOST_DIRECT_MAX
+    uint64_t host_direct_max = 4 << 20;   // 1-4 MB batches 1.6-2x faster direct, 16 MB even (profiles/r3/host_direct_sizes.log)
     int dec_tiles_per_block = 0;   // 0: grid from dec_blocks_per_cu alone; k: ceil(tiles / k) blocks (A/B)
     bool check = false;            // $WSG_CHECK=1: operand ranges validated before every device launch (debug)
     int dec_blocks_per_cu = 4096;  // k_decode grid cap: one 16 KiB tile per block up to 16 GiB of wire (tools/tune.py, round 2: C2 84.3 vs 85.1 us at 48 blocks/CU, 88.1 at two tiles per block; C3 ragged 0.685 vs 0.705 ms at 256, 0.783 at 48)
@@ -305,6 +309,8 @@ int wsg_create(int device, wsg_ctx** out)
     }
     if (const char* e = std::getenv("WSG_XOR_DIRECT_MAX"))   // A/B measurements (per-call path)
         c->xor_direct_max = std::strtoull(e, nullptr, 10);
+    if (const char* e = std::getenv("WSG_HOST_DIRECT_MAX"))   // A/B measurements (small host batches)
+        c->host_direct_max = std::strtoull(e, nullptr, 10);
     if (const char* e = std::getenv("WSG_DEC_TILES_PER_BLOCK")) {   // A/B measurements (tools/tune.py)
         const int v = std::atoi(e);
         if (v >= 0 && v <= 64)
@@ -828,6 +834,52 @@ int wsg_host_free(void* p)
     return WSG_OK;
 }
 
+namespace {
+
+// The batch's frame errors as the one-context call states them: a frame that
+// runs into the next one overlaps it (EINVAL) when its whole length lies
+// inside the wire; the status is the lowest-indexed bad frame's.
+int host_batch_status(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start, uint32_t n,
+                      wsg_recv_info* info)
+{
+    int first = WSG_OK;
+    for (uint32_t i = 0; i < n; ++i) {
+        wsg_recv_info& r = info[i];
+        if (r.error == WSG_ETRUNC && i + 1 < n && frame_start[i] < wire_len) {
+            wsg_recv_info h;
+            if (wsg_header_unpack(wire + frame_start[i], wire_len - frame_start[i], &h) == WSG_OK &&
+                h.len <= wire_len - frame_start[i] - h.hdr_len)
+                r.error = int8_t(WSG_EINVAL);
+        }
+        if (r.error && !first)
+            first = r.error;
+    }
+    if (first)   // re-arm the host paths' latch
+        WSG_HIP(hipMemset(c->d_err_host, 0xFF, sizeof(unsigned long long)));
+    return first;
+}
+
+// A small host batch in page-locked buffers (a read's frames, echo size):
+// k_decode reads the wire and writes the output where they are, over PCIe,
+// on the context's stream — one launch and one synchronize instead of the
+// pipeline's H2D + kernel + D2H on three streams with event hand-offs.
+int decode_host_direct(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start, uint32_t n,
+                       uint8_t* out, wsg_recv_info* info)
+{
+    wsg_ctx::Slot& sl = c->slots[0];
+    if (int rc = slot_reserve(sl, 0, n, false))
+        return rc;
+    std::memcpy(sl.h_fs, frame_start, size_t(n) * sizeof(uint64_t));
+    hipStream_t s = c->stream;
+    if (int rc = decode_launch(c, wire, wire_len, sl.h_fs, n, out, sl.h_info, s, c->d_err_host))
+        return rc;
+    WSG_HIP(hipStreamSynchronize(s));
+    std::memcpy(info, sl.h_info, size_t(n) * sizeof(wsg_recv_info));
+    return host_batch_status(c, wire, wire_len, frame_start, n, info);
+}
+
+} // namespace
+
 int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start,
                           uint32_t n, uint8_t* out, wsg_recv_info* info)
 {
@@ -844,6 +896,8 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
         if (const char* e = std::getenv("WSG_STAGE_MB"))
             seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
         const bool in_pinned = host_pinned(wire), out_pinned = host_pinned(out);
+        if (in_pinned && out_pinned && wire_len <= c->host_direct_max && aligned16(wire) && aligned16(out))
+            return decode_host_direct(c, wire, wire_len, frame_start, n, out, info);
 
         // segments: runs of whole frames of about seg_bytes; segment k covers wire
         // bytes [start of its first frame, start of the next segment's first frame)
@@ -926,22 +980,8 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
 
         // batch semantics: a frame that runs into the next segment's first frame
         // overlaps it (EINVAL), it is not truncated; and the status is the error
-        // of the lowest-indexed bad frame
-        int first = WSG_OK;
-        for (uint32_t i = 0; i < n; ++i) {
-            wsg_recv_info& r = info[i];
-            if (r.error == WSG_ETRUNC && i + 1 < n && frame_start[i] < wire_len) {
-                wsg_recv_info h;
-                if (wsg_header_unpack(wire + frame_start[i], wire_len - frame_start[i], &h) == WSG_OK &&
-                    h.len <= wire_len - frame_start[i] - h.hdr_len)
-                    r.error = int8_t(WSG_EINVAL);
-            }
-            if (r.error && !first)
-                first = r.error;
-        }
-        if (first)   // re-arm the pipeline's latch (every slot has drained)
-            WSG_HIP(hipMemset(c->d_err_host, 0xFF, sizeof(unsigned long long)));
-        return first;
+        // of the lowest-indexed bad frame (every slot has drained)
+        return host_batch_status(c, wire, wire_len, frame_start, n, info);
     } catch (...) {
         return WSG_ENOMEM;
     }
@@ -1015,6 +1055,21 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
         if (const char* e = std::getenv("WSG_STAGE_MB"))
             seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
         const bool in_pinned = host_pinned(payload), out_pinned = host_pinned(wire);
+        if (in_pinned && out_pinned && wire_off[n] <= c->host_direct_max && aligned16(wire) && n <= (1u << 20)) {
+            // a small batch in page-locked buffers (the frames a tick sends):
+            // the kernels read the payloads and write the frames where they
+            // are, one launch sequence and one synchronize
+            wsg_ctx::Slot& sl = c->slots[0];
+            if (int rc = slot_reserve_enc(sl, 0, wire_off[n], n, false))
+                return rc;
+            std::memcpy(sl.h_desc, desc, size_t(n) * sizeof(wsg_send_desc));
+            hipStream_t s = c->stream;
+            if (int rc = encode_launch(c, s, payload, sl.h_desc, n, wire, wire_off[n], sl.d_woff, sl.enc,
+                                       c->d_err_host))
+                return rc;
+            WSG_HIP(hipStreamSynchronize(s));
+            return WSG_OK;   // capacity was checked on the host: nothing for the latch to report
+        }
 
         // segments of whole frames, ~seg_bytes of wire each
         struct Seg {

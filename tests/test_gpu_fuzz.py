@@ -5,7 +5,8 @@ classes), opcodes (text/binary/continuation/close/ping/pong, RSV bits,
 unknown), mask flags, close statuses and misaligned sources.  Every batch
 goes through the device encode (piece or small-frame kernel, whichever the
 batch selects) and decode, out of place and in place, and through the
-host-staged pair; bytes, offsets, per-frame fields and status must equal the
+host-staged pair (pageable buffers: the staged pipeline; page-locked
+buffers: the direct path of small batches); bytes, offsets, per-frame fields and status must equal the
 oracle's.  Bit-exact, no tolerance.  $WSG_FUZZ_SEEDS widens the run."""
 import os
 
@@ -71,6 +72,19 @@ def test_fuzz_encode_decode_vs_oracle(codec, seed):
     rc_h, wire_h, off_h = codec.encode_batch_host(payload, desc)
     assert rc_h == 0 and np.array_equal(wire_h, wire_o) and np.array_equal(off_h, off_o)
     rc_h, out_h, info_h = codec.decode_batch_host(wire_o, fs)
+    assert rc_h == rc_o and np.array_equal(out_h, out_o)
+    for f in INFO_FIELDS:
+        assert np.array_equal(info_h[f], info_o[f]), f
+    # and with page-locked buffers both ways: batches up to 4 MiB take the
+    # direct path (the kernels read and write the host buffers in place)
+    pin_p = ca.pinned_empty(len(payload))
+    pin_p[:] = payload
+    pin_w = ca.pinned_empty(max(len(wire_o), 1))
+    rc_h, wire_h, off_h = codec.encode_batch_host(pin_p, desc, wire=pin_w)
+    assert rc_h == 0 and np.array_equal(wire_h, wire_o) and np.array_equal(off_h, off_o)
+    pin_in, pin_out = ca.pinned_empty(max(len(wire_o), 1)), ca.pinned_empty(max(len(wire_o), 1))
+    pin_in[: len(wire_o)] = wire_o
+    rc_h, out_h, info_h = codec.decode_batch_host(pin_in[: len(wire_o)], fs, out=pin_out)
     assert rc_h == rc_o and np.array_equal(out_h, out_o)
     for f in INFO_FIELDS:
         assert np.array_equal(info_h[f], info_o[f]), f

@@ -574,6 +574,42 @@ def test_decode_batch_host_segmented(codec, stage_mb, monkeypatch):
                 assert np.array_equal(info[fld], info_o[fld]), (variant, pinned, fld)
 
 
+@pytest.mark.parametrize("direct_max", ["4194304", "0"])
+def test_host_batches_pinned_errors(codec, direct_max, monkeypatch):
+    """Small host batches in page-locked buffers: the direct path (kernels on
+    the host buffers) and, with it off, the staged pipeline give the oracle's
+    bytes, fields and status, also for a truncated last frame and an overlap."""
+    monkeypatch.setenv("WSG_HOST_DIRECT_MAX", direct_max)
+    c = ca.Codec(0)   # the knob is read when the context is made
+    try:
+        rng = np.random.default_rng(77)
+        payload, desc = _mixed_desc(rng, 300, 0, 3000)
+        wire, off = oracle.encode_batch(payload, desc)
+        pin_p = ca.pinned_empty(len(payload))
+        pin_p[:] = payload
+        pin_w = ca.pinned_empty(len(wire) + 16)
+        rc, w2, off2 = c.encode_batch_host(pin_p, desc, wire=pin_w)
+        assert rc == 0 and np.array_equal(w2, wire) and np.array_equal(off2, off)
+        fs = off[:-1].copy()
+        for variant in ("ok", "trunc", "overlap"):
+            w, f = wire, fs
+            if variant == "trunc":
+                w = wire[:-5]
+            if variant == "overlap":
+                f = fs.copy()
+                f[150] += 1
+            rc_o, out_o, info_o = oracle.decode_batch(w, f)
+            src, dst = ca.pinned_empty(len(w) + 16), ca.pinned_empty(len(w) + 16)
+            src[: len(w)] = w
+            rc, out, info = c.decode_batch_host(src[: len(w)], f, out=dst)
+            assert rc == rc_o, variant
+            assert np.array_equal(out, out_o), variant
+            for fld in INFO_FIELDS:
+                assert np.array_equal(info[fld], info_o[fld]), (variant, fld)
+    finally:
+        c.close()
+
+
 def test_host_pipeline_keeps_caller_latch(codec):
     """A host-staged call between an async batch call and its wsg_sync must
     not clear (or add to) the error that async call latched."""
