@@ -12,8 +12,9 @@ of a node, framed output gathered to one rank) on the GPU.
   at world sizes 1, 2, 3 and 8 with every rank on the one GPU (device
   copies to the root), chunk sizes 1, 300, 700 and 1024, ragged jobs, other
   roots, ranks holding nothing, an encode error on a non-root rank; the
-  RCCL rank-per-process form at world size 1, the only RCCL group one GPU
-  allows; all against the oracle.
+  RCCL rank-per-process form at world size 1 over the real RCCL, and at
+  world sizes 2, 3 and 8 with ranks as threads over a loopback RCCL test
+  double (tests/cpp/loopback_rccl.cpp); all against the oracle.
 """
 import os
 import socket
@@ -283,6 +284,34 @@ def test_mgpu_world8_c5_shape_one_device():
         assert torch.equal(words, exp)
     finally:
         g.close()
+
+
+def test_mgpu_rank_form_world_n():
+    """The RCCL rank-per-process form at world 2, 3 and 8 on one GPU: ranks
+    are threads, RCCL is the loopback test double (tests/mgpu_rank_job.py);
+    the status and size all-gathers and the per-chunk Send/Recv into the root
+    against the oracle, other roots, empty ranks, an encode error on any
+    rank stopping every rank."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "tests", "cpp", "_build", "libloopback_rccl.so")
+    assert os.path.exists(lib), "build tests/cpp first (make -C tests/cpp)"
+    env = dict(os.environ, WSG_RCCL_LIB=lib)
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "mgpu_rank_job.py")], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(d["cases"]) == 16
+    for c in d["cases"]:
+        assert not c["hung"], c
+        if c["bad_rank"] is None:
+            assert c["rc"] == [0] * c["world"] and c["wire_ok"] and c["off_ok"], c
+        else:
+            assert c["rc"] == [ca.WSG_ENOMEM] * c["world"], c   # every rank learns of the failure
+    assert d["loopback_errors"] == 0   # every Send met its Recv, sizes agreed
 
 
 @pytest.mark.gpu
