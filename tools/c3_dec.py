@@ -4,7 +4,9 @@ frames, payload uniform in [128, 65536]) for several seeds, against uniform
 frames of the same total size (32 KiB + 64 B payload), so that what the
 ragged tables cost is told apart from the footprint.  Diagnostic only.
 
-usage: python tools/c3_dec.py [launches]
+usage: python tools/c3_dec.py [launches]   ($WSG_C3_WARM=seconds of warm-up
+launches before each measured series; a device copy of the same wire gives
+the jitter the footprint has without the codec)
 """
 import os
 import statistics
@@ -29,6 +31,19 @@ def encoded(c, payload, desc):
     return wire, woff
 
 
+WARM = float(os.environ.get("WSG_C3_WARM", "0"))   # seconds of launches before the measured ones
+
+
+def warm(fn):
+    import time
+
+    t_end = time.perf_counter() + WARM
+    while time.perf_counter() < t_end:
+        for _ in range(10):
+            fn()
+        torch.cuda.synchronize()
+
+
 def per_launch(c, wire, woff, launches, alt=None):
     out = torch.empty_like(wire)
     n = woff.numel() - 1
@@ -38,12 +53,29 @@ def per_launch(c, wire, woff, launches, alt=None):
         w, o = bufs[i % len(bufs)]
         c.decode_batch(w, o[:-1], out=out if w is wire else torch.empty_like(w), info=info)
     c.sync()
+    warm(lambda: c.decode_batch(wire, woff[:-1], out=out, info=info))
     outs = [out] + ([torch.empty_like(alt[0])] if alt is not None else [])
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(launches + 1)]
     ev[0].record()
     for i in range(launches):
         j = i % len(bufs)
         c.decode_batch(bufs[j][0], bufs[j][1][:-1], out=outs[j], info=info)
+        ev[i + 1].record()
+    torch.cuda.synchronize()
+    return [ev[i].elapsed_time(ev[i + 1]) for i in range(launches)]
+
+
+def copy_launch(src, launches):
+    """The same bytes through a plain device copy (hipMemcpyAsync), launch by
+    launch: the jitter the hardware shows for this footprint without the codec."""
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize()
+    warm(lambda: dst.copy_(src))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(launches + 1)]
+    ev[0].record()
+    for i in range(launches):
+        dst.copy_(src)
         ev[i + 1].record()
     torch.cuda.synchronize()
     return [ev[i].elapsed_time(ev[i + 1]) for i in range(launches)]
@@ -67,6 +99,9 @@ def main():
         show("ragged seed %d (same wire)" % seed, ms, alg)
         if seed == 3000:
             print("   per launch:", " ".join("%.3f" % x for x in ms), flush=True)
+            cp = copy_launch(wire, launches)
+            show("device copy of the same wire", cp, 2 * wire.numel())
+            print("   per launch:", " ".join("%.3f" % x for x in cp), flush=True)
             p2, d2 = wl.c3_batch(65536, 128, 65536, seed=seed + 100)
             alt = encoded(c, p2, d2)
             ms = per_launch(c, wire, woff, launches, alt=alt)
