@@ -88,3 +88,18 @@ def test_no_cpu_fallback_without_gpu():
 def test_strerror_names_codes():
     for code in (ca.WSG_OK, ca.WSG_EINVAL, ca.WSG_ETRUNC, ca.WSG_ENOMEM, ca.WSG_EHIP):
         assert ca.lib().wsg_strerror(code)
+
+
+def test_loopback_rccl_double_exports():
+    """The RCCL test double (tests/cpp/loopback_rccl.cpp) the rank-form GPU
+    test loads through $WSG_RCCL_LIB has every entry point wsg_mgpu.cpp's
+    rccl() looks up; without one of them the product would refuse it."""
+    path = os.path.join(ROOT, "tests", "cpp", "_build", "libloopback_rccl.so")
+    if not os.path.exists(path):
+        pytest.skip("tests/cpp not built")
+    src = open(os.path.join(ROOT, "cppserver_amd", "csrc", "wsg_mgpu.cpp")).read()
+    wanted = re.findall(r'sym\(r\.\w+, "(nccl\w+)"\)', src)
+    assert len(wanted) == 9
+    lib = ctypes.CDLL(path)
+    for name in wanted + ["loopback_rccl_errors"]:
+        assert hasattr(lib, name), name
