@@ -65,8 +65,17 @@ def dist_setup(args):
         # $WSG_BENCH_BACKEND=gloo rehearses the N-rank path on fewer GPUs
         # (ranks share devices round-robin); the real run is RCCL, one GPU per rank
         backend = os.environ.get("WSG_BENCH_BACKEND", "nccl")
-        if backend != "nccl":
+        share = backend != "nccl" or os.environ.get("WSG_BENCH_SHARE_DEVICES") == "1"
+        if share:
             local = local % torch.cuda.device_count()
+        if backend == "nccl" and share:
+            # RCCL over ranks sharing a GPU (a rehearsal on a smaller box): a host
+            # id per rank makes RCCL see one GPU per host and connect the ranks
+            # through its socket transport (it refuses two ranks of one host on
+            # one device); the real run leaves this unset
+            os.environ.setdefault("NCCL_HOSTID", "wsg-bench-rank-%d" % rank)
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+            os.environ.setdefault("NCCL_IB_DISABLE", "1")
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -887,9 +896,12 @@ def c5_capi_leg(world, rank, n_total=1 << 20, timeout=300):
 
     res = None
     if rank == 0:
+        env = dict(os.environ)
+        if os.environ.get("WSG_BENCH_SHARE_DEVICES") == "1" or os.environ.get("WSG_BENCH_BACKEND", "nccl") != "nccl":
+            env["WSG_MGPU_ONE_DEVICE"] = "1"   # the rehearsal's ranks share a GPU: so do the tool's
         try:
             r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mgpu_c5.py"), str(world), str(n_total)],
-                               capture_output=True, text=True, timeout=timeout)
+                               capture_output=True, text=True, timeout=timeout, env=env)
             if r.returncode == 0:
                 res = json.loads(r.stdout.strip().splitlines()[-1])
             else:

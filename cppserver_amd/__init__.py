@@ -553,7 +553,8 @@ class TxBatch:
         self._out = []
         _check(self._L.wsg_tx_flush(self._tx, self._sink, None, ctypes.byref(n)), "wsg_tx_flush")
         out, self._out = self._out, []
-        assert len(out) == n.value
+        if len(out) != n.value:
+            raise WSGError(WSG_EINVAL, "wsg_tx_flush: %d frames handed out, %d reported" % (len(out), n.value))
         return out
 
 

@@ -315,6 +315,36 @@ def test_mgpu_rank_form_world_n():
 
 
 @pytest.mark.gpu
+def test_mgpu_rank_form_real_rccl_processes():
+    """The RCCL rank form over the REAL RCCL, one process per rank, at world 2
+    and 3 on the one GPU (tests/mgpu_rank_procs.py: a host id per rank, so
+    RCCL connects the ranks through its socket transport instead of refusing
+    two ranks on one device): ncclCommInitRank, the status / size
+    all-gathers and the grouped per-chunk Send/Recv, process against
+    process; the root's wire and offsets vs the oracle, an encode error on
+    rank 1 reaching every rank."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "mgpu_rank_procs.py")], capture_output=True,
+                       text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(d["cases"]) == 9
+    for c in d["cases"]:
+        assert not c["hung"], c
+        rcs = [x.get("rc") for x in c["ranks"]]
+        if c["bad_rank"] is None:
+            assert rcs == [0] * c["world"], c
+            top = c["ranks"][c["root"]]
+            assert top["wire_ok"] and top["off_ok"], c
+        else:
+            assert rcs == [ca.WSG_ENOMEM] * c["world"], c
+
+
+@pytest.mark.gpu
 def test_mgpu_c5_tool_world1():
     """tools/mgpu_c5.py (the C-ABI leg bench.py runs at N > 1) at world 1 on
     a reduced job: encode + gather through wsg_mgpu_create, root check."""
