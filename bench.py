@@ -19,6 +19,7 @@ frames, C4 fan-out of one 4 KiB payload to 10000 keys, C5 the whole 1 Mi x
 16 KiB job on this GPU.  --config c3|c4|c5 makes one of them the headline.
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -1014,15 +1015,26 @@ def timed_region(w, steps, world, device):
     e1.record()
     barrier(world)
     torch.cuda.synchronize()
-    with marker("bench.%s.timed" % w.cfg):
-        t0 = time.perf_counter()
-        e0.record()
-        for _ in range(steps):
-            w.step()
-        e1.record()
-        torch.cuda.synchronize()
+    # no Python garbage collection inside the region (a full collection of the
+    # interpreter's objects is a host stall of milliseconds, unrelated to the
+    # path measured); what was collectable goes now
+    gc.collect()
+    gc.disable()
+    try:
+        with marker("bench.%s.timed" % w.cfg):
+            t0 = time.perf_counter()
+            e0.record()
+            for _ in range(steps):
+                w.step()
+            e1.record()
+            t_sub = time.perf_counter()
+            torch.cuda.synchronize()
+            # the clock stops at this rank's synchronize; the closing barrier
+            # only lines the ranks up again (max over ranks takes the slowest)
+            elapsed = time.perf_counter() - t0
+    finally:
+        gc.enable()
     barrier(world)
-    elapsed = time.perf_counter() - t0
     region_ms = e0.elapsed_time(e1)
     if single:
         kern, spread = [(region_ms, steps)], [None]
@@ -1039,7 +1051,7 @@ def timed_region(w, steps, world, device):
     elapsed = max_over_ranks(elapsed, world, device)
     avgs = [max_over_ranks(ms / max(k, 1), world, device) for ms, k in kern]
     return {"elapsed": elapsed, "region_event_ms": region_ms, "kernel_avg_ms": avgs, "timing": note,
-            "minmax": spread}
+            "minmax": spread, "submit_ms": (t_sub - t0) * 1e3}
 
 
 def config_obj(args, cfg, codec, rank, world, device, steps, warmup, cpu):
@@ -1168,7 +1180,12 @@ def main():
                            r["minmax"][1])
         roof = dict(dec, halves=[roof, dec])
 
-    extras = {"event_ms_per_step": round(r["region_event_ms"] / args.steps, 4)}
+    extras = {"event_ms_per_step": round(r["region_event_ms"] / args.steps, 4),
+              # where the wall clock's excess over the events goes: the host's
+              # time to submit the region (launches queue behind a busy GPU
+              # after the first) and the rest, first-launch latency + wake-up
+              "region_host": {"submit_ms": round(r["submit_ms"], 4),
+                              "wall_minus_events_ms": round(elapsed * 1e3 - r["region_event_ms"], 4)}}
     if w.cfg == "c5" and world > 1:
         extras["gather"] = gather_leg(w, world, rank, device)
     if w.cfg == "c2" and world > 1 and not args.no_extras:

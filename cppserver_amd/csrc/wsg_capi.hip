@@ -705,6 +705,20 @@ bool host_pinned(const void* p)
     return a.type == hipMemoryTypeHost;
 }
 
+// Page-locked AND mapped at the same address on the device, so a kernel may
+// take the host pointer as it is (hipHostMalloc memory).  Memory registered
+// with hipHostRegister can have another device address; such buffers take
+// the staged pipeline (hipMemcpyAsync handles any host pointer).
+bool host_direct(const void* p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost && a.devicePointer == p;
+}
+
 int slot_init(wsg_ctx::Slot& sl)
 {
     if (sl.stream)
@@ -854,8 +868,12 @@ int host_batch_status(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const 
         if (r.error && !first)
             first = r.error;
     }
-    if (first)   // re-arm the host paths' latch
-        WSG_HIP(hipMemset(c->d_err_host, 0xFF, sizeof(unsigned long long)));
+    if (first) {   // re-arm the host paths' latch, landed before the next call's kernels
+        // (a plain hipMemset goes to the null stream, which the context's
+        // non-blocking streams do not wait for, and may return before it lands)
+        WSG_HIP(hipMemsetAsync(c->d_err_host, 0xFF, sizeof(unsigned long long), c->stream));
+        WSG_HIP(hipStreamSynchronize(c->stream));
+    }
     return first;
 }
 
@@ -896,7 +914,8 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
         if (const char* e = std::getenv("WSG_STAGE_MB"))
             seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
         const bool in_pinned = host_pinned(wire), out_pinned = host_pinned(out);
-        if (in_pinned && out_pinned && wire_len <= c->host_direct_max && aligned16(wire) && aligned16(out))
+        if (in_pinned && out_pinned && wire_len <= c->host_direct_max && aligned16(wire) && aligned16(out) &&
+            host_direct(wire) && host_direct(out))
             return decode_host_direct(c, wire, wire_len, frame_start, n, out, info);
 
         // segments: runs of whole frames of about seg_bytes; segment k covers wire
@@ -1055,7 +1074,8 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
         if (const char* e = std::getenv("WSG_STAGE_MB"))
             seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
         const bool in_pinned = host_pinned(payload), out_pinned = host_pinned(wire);
-        if (in_pinned && out_pinned && wire_off[n] <= c->host_direct_max && aligned16(wire) && n <= (1u << 20)) {
+        if (in_pinned && out_pinned && wire_off[n] <= c->host_direct_max && aligned16(wire) && n <= (1u << 20) &&
+            host_direct(wire) && (payload_len == 0 || host_direct(payload))) {
             // a small batch in page-locked buffers (the frames a tick sends):
             // the kernels read the payloads and write the frames where they
             // are, one launch sequence and one synchronize

@@ -431,7 +431,9 @@ int encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* 
         for (size_t i = 0; i < nl; ++i)
             if (g->local[i].rank == root && d_out_off) {
                 WSG_HIP(hipSetDevice(g->local[i].device));
-                WSG_HIP(hipMemset(d_out_off, 0, sizeof(uint64_t)));
+                hipStream_t s = static_cast<hipStream_t>(wsg_stream(g->local[i].ctx));
+                WSG_HIP(hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), s));
+                WSG_HIP(hipStreamSynchronize(s));
             }
         if (times)
             times[0] = times[1] = 0.0;
@@ -455,7 +457,11 @@ int encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* 
         for (Local& l : g->local) {
             WSG_HIP(hipSetDevice(l.device));
             const uint64_t mine = uint64_t(uint32_t(-status));
-            WSG_HIP(hipMemcpy(l.d_status, &mine, sizeof(uint64_t), hipMemcpyHostToDevice));
+            // on the stream the all-gather runs on, landed before it (host
+            // data into device memory by a plain hipMemcpy is not ordered
+            // with the context's non-blocking stream)
+            WSG_HIP(hipMemcpyAsync(l.d_status, &mine, sizeof(uint64_t), hipMemcpyHostToDevice, stream_of(l)));
+            WSG_HIP(hipStreamSynchronize(stream_of(l)));
         }
         WSG_NCCL(r->GroupStart());
         for (Local& l : g->local)
@@ -545,7 +551,9 @@ int encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* 
         for (size_t i = 0; i < nl; ++i) {
             Local& l = g->local[i];
             WSG_HIP(hipSetDevice(l.device));
-            WSG_HIP(hipMemcpy(l.d_sizes, sizes[i].data(), maxq * sizeof(uint64_t), hipMemcpyHostToDevice));
+            WSG_HIP(hipMemcpyAsync(l.d_sizes, sizes[i].data(), maxq * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                   stream_of(l)));
+            WSG_HIP(hipStreamSynchronize(stream_of(l)));
         }
         WSG_NCCL(r->GroupStart());
         for (Local& l : g->local)
@@ -568,8 +576,12 @@ int encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* 
     if (root_l && total > out_cap)
         fail(WSG_ENOMEM);
     if (root_l && !status) {
+        // on the root's stream (k_rebase_offsets reads it there), landed
+        // before the host vector goes
         if (hipSetDevice(root_l->device) != hipSuccess ||
-            hipMemcpy(root_l->d_goff, goff.data(), goff.size() * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess)
+            hipMemcpyAsync(root_l->d_goff, goff.data(), goff.size() * sizeof(uint64_t), hipMemcpyHostToDevice,
+                           stream_of(*root_l)) != hipSuccess ||
+            hipStreamSynchronize(stream_of(*root_l)) != hipSuccess)
             fail(WSG_EHIP);
     }
     // a short root buffer must stop every rank before the transfers, or the

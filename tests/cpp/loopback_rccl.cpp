@@ -13,7 +13,11 @@
 // collective of every rank and places rank k's block at k * count.  Each
 // group is completed synchronously at ncclGroupEnd (the posting streams are
 // drained first) — the test checks placement, pairing and ordering, not
-// overlap.  A mismatch (a Recv with no Send, a size disagreement, a Send
+// overlap.  Copies run on the receiving rank's stream and are complete when
+// the group returns (a plain hipMemcpy between device buffers may return
+// before the copy lands, unordered with the product's non-blocking streams:
+// a kernel the root queued after the Recv then read stale offsets, seen once
+// on the box).  A mismatch (a Recv with no Send, a size disagreement, a Send
 // nobody received within 60 s, an AllGather count disagreement) fails the
 // group on the rank that sees it with ncclInvalidUsage and is counted in
 // loopback_rccl_errors().
@@ -153,7 +157,11 @@ ncclResult_t run_group(ncclComm* c, const std::vector<Op>& ops)
                 s = box.front();
                 box.pop_front();
             }
-            const bool ok = s->bytes == op.bytes && hipMemcpy(op.dst, s->src, op.bytes, hipMemcpyDefault) == hipSuccess;
+            // on the receiver's stream, complete before the group returns (the
+            // product orders its next launch on that stream after the Recv)
+            const bool ok = s->bytes == op.bytes &&
+                            hipMemcpyAsync(op.dst, s->src, op.bytes, hipMemcpyDefault, op.stream) == hipSuccess &&
+                            hipStreamSynchronize(op.stream) == hipSuccess;
             bad = bad || !ok;
             std::lock_guard<std::mutex> lk(g->m);
             s->ok = ok;
@@ -168,10 +176,12 @@ ncclResult_t run_group(ncclComm* c, const std::vector<Op>& ops)
             for (int k = 0; k < world; ++k) {
                 const Op& src = g->ag_src[size_t(k)];
                 if (src.kind != Op::ALLGATHER || src.bytes != op.bytes ||
-                    hipMemcpy(static_cast<uint8_t*>(op.dst) + size_t(k) * op.bytes, src.src, op.bytes,
-                              hipMemcpyDefault) != hipSuccess)
+                    hipMemcpyAsync(static_cast<uint8_t*>(op.dst) + size_t(k) * op.bytes, src.src, op.bytes,
+                                   hipMemcpyDefault, op.stream) != hipSuccess)
                     bad = true;
             }
+            if (hipStreamSynchronize(op.stream) != hipSuccess)
+                bad = true;
             barrier(g);   // every rank has copied before any posts its next block
         }
     }

@@ -610,6 +610,46 @@ def test_host_batches_pinned_errors(codec, direct_max, monkeypatch):
         c.close()
 
 
+def test_host_batches_registered_memory(codec):
+    """Host batches in memory page-locked with hipHostRegister (a server's own
+    socket buffers registered in place): such memory may have another device
+    address, so the direct small-batch path must not hand the host pointer
+    to a kernel; results are the oracle's either way, at buffer offsets too."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    rng = np.random.default_rng(78)
+    payload, desc = _mixed_desc(rng, 200, 0, 3000)
+    wire, off = oracle.encode_batch(payload, desc)
+    fs = off[:-1].copy()
+    rc_o, out_o, info_o = oracle.decode_batch(wire, fs)
+    need = 3 * (len(wire) + len(payload)) + (1 << 16)
+    raw = np.zeros(need + 8192, dtype=np.uint8)
+    base = raw.ctypes.data + (-raw.ctypes.data) % 4096
+    region = raw[base - raw.ctypes.data: base - raw.ctypes.data + need]
+    assert hip.hipHostRegister(ctypes.c_void_p(base), ctypes.c_size_t(need), 0) == 0
+    try:
+        for shift in (0, 4096 + 16):
+            a = shift
+            src = region[a: a + len(wire)]
+            a += (len(wire) + 15) // 16 * 16
+            dst = region[a: a + len(wire)]
+            a += (len(wire) + 15) // 16 * 16
+            pl = region[a: a + len(payload)]
+            a += (len(payload) + 15) // 16 * 16
+            wout = region[a: a + len(wire)]
+            src[:] = wire
+            rc, out, info = codec.decode_batch_host(src, fs, out=dst)
+            assert rc == rc_o and np.array_equal(out, out_o), shift
+            for fld in INFO_FIELDS:
+                assert np.array_equal(info[fld], info_o[fld]), (shift, fld)
+            pl[:] = payload
+            rc, w2, off2 = codec.encode_batch_host(pl, desc, wire=wout)
+            assert rc == 0 and np.array_equal(w2, wire) and np.array_equal(off2, off), shift
+    finally:
+        hip.hipHostUnregister(ctypes.c_void_p(base))
+
+
 def test_host_pipeline_keeps_caller_latch(codec):
     """A host-staged call between an async batch call and its wsg_sync must
     not clear (or add to) the error that async call latched."""
