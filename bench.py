@@ -1017,8 +1017,9 @@ def timed_region(w, steps, world, device):
     torch.cuda.synchronize()
     # no Python garbage collection inside the region (a full collection of the
     # interpreter's objects is a host stall of milliseconds, unrelated to the
-    # path measured); what was collectable goes now
-    gc.collect()
+    # path measured).  Not gc.collect() here: a collection right before t0
+    # leaves the host's caches cold and adds ~100 us to a 20-step region
+    # (tools/gap3.py: wall - events 22 us without it, 119 us with it)
     gc.disable()
     try:
         with marker("bench.%s.timed" % w.cfg):
