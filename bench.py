@@ -1090,6 +1090,14 @@ def config_obj(args, cfg, codec, rank, world, device, steps, warmup, cpu):
         obj["roofline"] = rf
         if cfg == "c3":
             obj["k_decode_per_launch"] = decode_launches(w)
+        if cfg == "c4":
+            # the ws_multicast tick's form: 16 such messages in ONE launch
+            # (wsg_fanout_encode_many), where one 41 MB fan-out is too short
+            # to reach the write rate on its own
+            many = fanout_many_leg(w)
+            per_msg = w.alg_bytes   # one message: frames + payload + keys
+            many["frac"] = round(per_msg / (many["us_per_message"] * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
+            obj["multicast_tick_16"] = many
         if cpu is not None and rank == 0:
             c1, cn = cpu_baseline(w, args.cpu_seconds * 0.6, cpu)
             obj["cpu_baseline"], obj["cpu_baseline_mt"] = c1, cn
