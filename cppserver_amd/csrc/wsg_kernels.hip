@@ -51,7 +51,7 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #define WSG_DIAG 0   // 5: timing-only diagnostic build of k_decode (every tile streams; tools/)
 #endif
 #ifndef WSG_DIAG_FAN
-#define WSG_DIAG_FAN 0   // timing-only fan-out diagnostics: 1 no key loads, 2 no payload loads, 4 stores only, 8 no edge blocks; period path: 16 no template loads, 32 no key loads, 64 no stores
+#define WSG_DIAG_FAN 0   // timing-only fan-out diagnostics: 1 no key loads, 2 no payload loads, 4 stores only, 8 no edge blocks; period path: 16 no template loads, 32 no key loads, 64 no stores, 128 prologue only, 256 empty
 #endif
 #ifndef WSG_DIAG_NOINFO
 #define WSG_DIAG_NOINFO 0   // timing-only: k_decode without its per-frame info slice (tools/)
@@ -70,6 +70,12 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #endif
 #ifndef WSG_FAN_PERIOD
 #define WSG_FAN_PERIOD 1   // fan-out: period path (k_fanout_period) where the frame size allows; 0 = flat kernel only
+#endif
+#ifndef WSG_FAN_PRO
+#define WSG_FAN_PRO 1   // fan-out period path prologue (A/B, tools/c4_ab.py): 1 all kernel arguments loaded in one round, 2 both payload windows issued together branch-free, 4 early exit past the last row
+#endif
+#ifndef WSG_FAN_UNROLL
+#define WSG_FAN_UNROLL 1   // fan-out period path: passes per loop iteration (A/B)
 #endif
 #ifndef WSG_FAN_KV
 #define WSG_FAN_KV 2   // fan-out period path: key registers per lane (64 pass-window slots each)
@@ -1597,15 +1603,71 @@ __device__ __forceinline__ void fan_tm(const uint8_t* __restrict__ payload, uint
         t |= fan_window(payload, len, int64_t(o) - int64_t(f.data0)) & (low_bytes(hi) & ~low_bytes(lo));
 }
 
+// fan_tm for two chunk offsets at once (a chunk's and a frame start's):
+// both payload windows' loads are issued before either is used, so they
+// come back in one memory round trip (fan_tm's own branches made the
+// compiler wait for the first pair before issuing the second)
+struct FanWin {
+    v4u lo, hi;
+    uint32_t s;
+};
+__device__ __forceinline__ FanWin fan_window_issue(const uint8_t* __restrict__ payload, uint64_t len, int64_t c)
+{
+    // branch-free: each load is issued unconditionally from a block clamped
+    // into the payload's own aligned blocks, and zeroed where fan_window
+    // would not have loaded it (a load under a branch made the compiler
+    // copy its result inside the branch, i.e. wait for it there); the
+    // period path has len >= 1 (host: G >= 64 needs frames of >= 512 B)
+    FanWin w;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(payload);
+    w.s = uint32_t((base + uint64_t(c)) & 15u);
+    const int64_t r0 = c - int64_t(w.s);   // aligned block holding byte c, relative to payload
+    const int64_t n = int64_t(len);
+    const int64_t first = -int64_t(base & 15u);                                        // block of byte 0
+    const int64_t last = int64_t(((base + len - 1) & ~uintptr_t(15)) - base);         // block of byte len - 1
+    const int64_t r1 = r0 + 16;
+    const bool ok_lo = r0 < n && r0 + 16 > 0;
+    const bool ok_hi = r1 < n && r1 + 16 > 0;   // (unused at s = 0: funnel(lo, hi, 0) = lo)
+    const v4u a = ld16(payload + (r0 < first ? first : r0 > last ? last : r0));
+    const v4u b = ld16(payload + (r1 < first ? first : r1 > last ? last : r1));
+    const v4u z = {0, 0, 0, 0};
+    w.lo = ok_lo ? a : z;
+    w.hi = ok_hi ? b : z;
+    return w;
+}
+__device__ __forceinline__ void fan_tm_finish(const FanWin& w, const FanGeom& f, uint64_t fsize, uint64_t o, v4u& t,
+                                              v4u& m)
+{
+    const uint64_t hi = fsize - o < CHUNK ? fsize - o : CHUNK;
+    const uint64_t kl = o < f.kpos ? f.kpos - o : 0;
+    const uint64_t lo = o < f.data0 ? f.data0 - o : 0;
+    m = low_bytes(hi) & ~low_bytes(kl);
+    t = shr_bytes(f.hp0, o);
+    // no `if (lo < hi)`: the byte mask is empty then, and a branch here let
+    // the compiler sink the loads into it, behind a wait
+    t |= funnel(w.lo, w.hi, w.s) & (low_bytes(hi) & ~low_bytes(lo));
+}
+
 template <int P>
 __global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict__ payload0, uint64_t len,
                                                       const uint32_t* __restrict__ keys, uint32_t k, uint8_t opcode,
                                                       uint32_t mask, uint64_t fsize, uint32_t G, uint32_t dm,
-                                                      uint8_t* __restrict__ wire0, const FanMsgs msgs, v4u hp0)
+                                                      uint8_t* __restrict__ wire0, const FanMsgs msgs, v4u hp0,
+                                                      uint32_t nwaves)
 {
     constexpr int KW = 2 * P;   // keys per pass: the row spans <= 2 groups (G >= 64)
-    const uint8_t* __restrict__ payload = payload0 + msgs.src[blockIdx.y];
-    uint8_t* __restrict__ wire = wire0 + msgs.dst[blockIdx.y];
+    if (WSG_DIAG_FAN & 256)     // diagnostic: the launch of the grid alone
+        return;
+    const uint64_t src_off = msgs.src[blockIdx.y], dst_off = msgs.dst[blockIdx.y];
+    // every kernel argument in SGPRs before anything else: left to the
+    // compiler, the argument loads came in five dependent rounds (each
+    // waiting on the last), a visible share of a 9 us kernel; this empty
+    // asm consumes them all, so they are issued together and waited once
+    if (WSG_FAN_PRO & 1)
+        asm volatile("" ::"s"(payload0), "s"(len), "s"(keys), "s"(k), "s"(fsize), "s"(G), "s"(dm), "s"(wire0),
+                     "s"(nwaves), "s"(src_off), "s"(dst_off), "s"(uint32_t(opcode)), "s"(mask));
+    const uint8_t* __restrict__ payload = payload0 + src_off;
+    uint8_t* __restrict__ wire = wire0 + dst_off;
     FanGeom f;   // fan_geom() with the header bytes from the host (hp0)
     f.g = send_geom(opcode, mask != 0, len, 0);
     f.data0 = f.g.hdr + f.g.prefix;
@@ -1615,17 +1677,32 @@ __global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict_
     const uint64_t total = fsize * k;
     const uint64_t chunks = (total + CHUNK - 1) / CHUNK;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wpb = blockDim.x / 64;              // 1, 2 or 4 waves per block (host: W % wpb == 0)
-    // wave-uniform (readfirstlane): the write-through stores' buffer resource
-    // must sit in SGPRs, or every store becomes a waterfall loop
-    const uint64_t row0 = (uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x / 64)) * 64;
-    const uint64_t rstep = uint64_t(gridDim.x) * wpb * 64;   // W rows: a multiple of G (dm groups)
-    if (row0 >= chunks)
+    // one wave per block, W = nwaves of them (a kernel argument, not
+    // gridDim: the dispatch packet is one more memory read before the first
+    // store); rows are wave-uniform, so the write-through stores' buffer
+    // resource sits in SGPRs (else every store becomes a waterfall loop)
+    const uint64_t row0 = uint64_t(blockIdx.x) * 64;
+    const uint64_t rstep = uint64_t(nwaves) * 64;   // W rows: a multiple of G (dm groups)
+    if ((WSG_FAN_PRO & 4) && row0 >= chunks)   // a wave past the last row (its loads are guarded anyway)
         return;
-    const uint64_t m0 = (row0 >> 32) ? row0 / G : uint64_t(uint32_t(row0) / G);   // first group of pass 0
+    const uint64_t m0 = uint32_t(row0) / G;              // first group of pass 0 (host: W < 2^22, row0 < 2^28)
     const uint32_t jw = uint32_t(row0 - m0 * G);         // group position of lane 0
     const uint32_t dl = (jw + lane) >= G ? 1u : 0u;      // lane's group: m0 + dl (+ it * dm)
     const uint32_t j = jw + lane - dl * G;
+
+    // keys of every pass: slot it * KW + q -> key P * (m0 + it * dm) + q
+    // (host: passes * KW <= 64 * WSG_FAN_KV).  Issued before the template's
+    // payload loads, so the two arrive together: the kernel is short (41 MB
+    // at C4), and a second dependent memory round trip before the first
+    // store was a visible share of it
+    uint32_t kv[WSG_FAN_KV];
+#pragma unroll
+    for (int h = 0; h < WSG_FAN_KV; ++h) {
+        const uint32_t s = uint32_t(h) * 64 + lane;
+        const uint64_t it = s / KW;
+        const uint64_t idx = uint64_t(P) * (m0 + it * dm) + (s % KW);
+        kv[h] = (WSG_DIAG_FAN & 32) ? uint32_t(idx) : (row0 + it * rstep < chunks && idx < k) ? keys[idx] : 0u;
+    }
 
     // template of chunk j: its frame-a bytes, and the next frame's from byte
     // `split` on (the first 16 bytes of a frame: the same for every lane)
@@ -1636,32 +1713,33 @@ __global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict_
         qa += o >= uint64_t(q) * fsize ? 1u : 0u;
     const uint64_t r = o - uint64_t(qa) * fsize;
     v4u t, ma, mb = {0, 0, 0, 0};
+    // a frame's first 16 bytes (the same for every lane), built by every
+    // lane so that its payload loads go out with the chunk's own instead of
+    // in a second round behind them; used where a frame starts in the chunk
+    const uint64_t split = fsize - r;                    // the next frame starts at chunk byte `split`
+    if (WSG_FAN_PRO & 2) {
+        v4u t0, m0v;
+        const FanWin wa = fan_window_issue(payload, len, int64_t(r) - int64_t(f.data0));
+        const FanWin wb = fan_window_issue(payload, len, -int64_t(f.data0));
+        fan_tm_finish(wb, f, fsize, 0, t0, m0v);
+        fan_tm_finish(wa, f, fsize, r, t, ma);
+        t |= shl_bytes(t0, split);                       // (zero unless split < CHUNK; no branch, see above)
+        mb = shl_bytes(m0v, split);
+    } else {
+        fan_tm(payload, len, f, fsize, r, t, ma);
+        if (split < CHUNK) {
+            v4u t0, m0v;
+            fan_tm(payload, len, f, fsize, 0, t0, m0v);
+            t |= shl_bytes(t0, split);
+            mb = shl_bytes(m0v, split);
+        }
+    }
     if (WSG_DIAG_FAN & 16) {
         t = v4u{j, 1, 2, 3};
         ma = v4u{~0u, ~0u, ~0u, ~0u};
-    } else {
-        fan_tm(payload, len, f, fsize, r, t, ma);
-    }
-    const uint64_t split = fsize - r;                    // the next frame starts at chunk byte `split`
-    if (split < CHUNK) {
-        v4u t0, m0v;
-        fan_tm(payload, len, f, fsize, 0, t0, m0v);
-        t |= shl_bytes(t0, split);
-        mb = shl_bytes(m0v, split);
     }
     const uint32_t pa = uint32_t(r - f.g.hdr), pb = uint32_t(0u - uint32_t(split) - f.g.hdr);
     const uint32_t ia = P * dl + qa;                     // key slots of this pass's window
-
-    // keys of every pass: slot it * KW + q -> key P * (m0 + it * dm) + q
-    // (host: passes * KW <= 64 * WSG_FAN_KV)
-    uint32_t kv[WSG_FAN_KV];
-#pragma unroll
-    for (int h = 0; h < WSG_FAN_KV; ++h) {
-        const uint32_t s = uint32_t(h) * 64 + lane;
-        const uint64_t it = s / KW;
-        const uint64_t idx = uint64_t(P) * (m0 + it * dm) + (s % KW);
-        kv[h] = (WSG_DIAG_FAN & 32) ? uint32_t(idx) : (row0 + it * rstep < chunks && idx < k) ? keys[idx] : 0u;
-    }
 
     // Pass loop, kept lean (it is most of the kernel's instructions): running
     // row / pointer / shuffle-address registers instead of per-pass products,
@@ -1673,7 +1751,13 @@ __global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict_
     uint8_t* wrow = wire + row0 * CHUNK;
     const uint64_t wstep = rstep * CHUNK;
     uint32_t addr = ia * 4;                                 // shuffle address of key slot ia of pass 0
-#pragma unroll 1
+    if (WSG_DIAG_FAN & 128) {   // diagnostic: the prologue alone (its results kept live)
+        const v4u w = t ^ ma ^ mb ^ v4u{kv[0], kv[WSG_FAN_KV - 1], addr, 0};
+        if ((w[0] & w[1] & w[2] & w[3]) == 0xA5C3E1F7u && row0 + lane < chunks)
+            st16nt(wire + (row0 + lane) * CHUNK, w);
+        return;
+    }
+#pragma unroll WSG_FAN_UNROLL
     for (uint32_t it = 0; row < chunks; ++it) {
         const uint32_t slot = it * KW;                      // wave-uniform; KW divides 64
         uint32_t kreg = kv[0];
@@ -1839,7 +1923,7 @@ bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_
     if (W > (1u << 22))
         return false;
     const uint32_t dm = uint32_t(W * 64 / G);
-    const uint64_t wpb = 1;   // waves per block: one (4-wave blocks measured 8 % slower at C4)
+    // waves per block: one (4-wave blocks measured 8 % slower at C4)
     // header bytes before the key (<= 10), the same in every frame
     const SendGeom sg = send_geom(opcode, mask != 0, len, 0);
     const uint32_t kpos = sg.hdr - (mask ? 4u : 0u);
@@ -1849,13 +1933,16 @@ bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_
     const v4u hp0 = v4u{hw[0], hw[1], hw[2], hw[3]};
     switch (P) {
     case 1:
-        k_fanout_period<1><<<dim3(uint32_t(W / wpb), nmsgs), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire, msgs, hp0);
+        k_fanout_period<1><<<dim3(uint32_t(W), nmsgs), 64, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm,
+                                                               wire, msgs, hp0, uint32_t(W));
         break;
     case 2:
-        k_fanout_period<2><<<dim3(uint32_t(W / wpb), nmsgs), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire, msgs, hp0);
+        k_fanout_period<2><<<dim3(uint32_t(W), nmsgs), 64, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm,
+                                                               wire, msgs, hp0, uint32_t(W));
         break;
     default:
-        k_fanout_period<4><<<dim3(uint32_t(W / wpb), nmsgs), uint32_t(64 * wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm, wire, msgs, hp0);
+        k_fanout_period<4><<<dim3(uint32_t(W), nmsgs), 64, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm,
+                                                               wire, msgs, hp0, uint32_t(W));
         break;
     }
     *err = hipGetLastError();
