@@ -42,7 +42,12 @@ struct wsg_ctx {
     int dec_tiles_per_block = 0;   // 0: grid from dec_blocks_per_cu alone; k: ceil(tiles / k) blocks (A/B)
     bool check = false;            // $WSG_CHECK=1: operand ranges validated before every device launch (debug)
     int dec_blocks_per_cu = 4096;  // k_decode grid cap: one 16 KiB tile per block up to 16 GiB of wire (tools/tune.py, round 2: C2 84.3 vs 85.1 us at 48 blocks/CU, 88.1 at two tiles per block; C3 ragged 0.685 vs 0.705 ms at 256, 0.783 at 48)
-    int fan_waves_per_cu = 8;    // fan-out period path: waves per CU (tools/tune_enc.py CFG=c4: 8 best of 4-32)
+    int fan_waves_per_cu = 6;    // fan-out period path: waves per CU (tools/c4_ab.py, graph-replayed C4: 6 -> 8.10 us, 4 -> 8.16, 8 -> 8.32)
+    // fan-out period path: waves per workgroup (A/B $WSG_FAN_WPB; one-wave
+    // workgroups measured best: C4 8.5 us against 9.3 at 4 and 9.0 at 8-16,
+    // tools/c4_ab.py with graph-replayed launches; an empty kernel of that
+    // grid is 1.65 us either way)
+    int fan_wpb = 1;
     uint64_t small_avg = wsg::SMALL_AVG;   // batch encode: k_encode_small when wire_cap <= n * small_avg
     unsigned long long* d_err = nullptr;        // latch of the caller-visible async entry points (wsg_sync)
     unsigned long long* d_err_host = nullptr;   // latch of the host-staged pipelines (their own status)
@@ -325,6 +330,11 @@ int wsg_create(int device, wsg_ctx** out)
     }
     if (const char* e = std::getenv("WSG_ENC_LAUNCH_PIECES"))   // A/B measurements (tools/c5_split.py)
         c->enc_launch_pieces = std::strtoull(e, nullptr, 10);
+    if (const char* e = std::getenv("WSG_FAN_WPB")) {   // A/B measurements (tools/c4_ab.py)
+        const int v = std::atoi(e);
+        if (v == 1 || v == 2 || v == 4 || v == 8 || v == 16)
+            c->fan_wpb = v;
+    }
     if (const char* e = std::getenv("WSG_FAN_WAVES_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
         const int v = std::atoi(e);
         if (v > 0 && v <= 64)
@@ -582,7 +592,7 @@ int fanout_many(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, const uint6
                 g.dst[q] = wire_off[members[at + q]];
             }
             hipError_t perr = hipSuccess;
-            if (wsg::launch_fanout_period(s, c->num_cus, c->fan_waves_per_cu, d_payload, len[i], d_keys, k, opcode[i],
+            if (wsg::launch_fanout_period(s, c->num_cus, c->fan_waves_per_cu, c->fan_wpb, d_payload, len[i], d_keys, k, opcode[i],
                                           mask ? 1u : 0u, fsize, d_wire, g, cnt, &perr)) {
                 WSG_HIP(perr);
             } else {

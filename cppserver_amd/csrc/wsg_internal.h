@@ -80,7 +80,7 @@ struct FanMsgs {
 };
 // Period-path fan-out of nmsgs (<= FAN_MSGS) messages of one geometry; false:
 // the frame size does not suit it (the caller takes launch_fanout per message).
-bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_t* payload, uint64_t len,
+bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, int wpb, const uint8_t* payload, uint64_t len,
                           const uint32_t* keys, uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize,
                           uint8_t* wire, const FanMsgs& msgs, uint32_t nmsgs, hipError_t* err);
 hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64_t len, const uint32_t* keys,

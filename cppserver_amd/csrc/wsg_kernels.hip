@@ -74,6 +74,9 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_FAN_PRO
 #define WSG_FAN_PRO 1   // fan-out period path prologue (A/B, tools/c4_ab.py): 1 all kernel arguments loaded in one round, 2 both payload windows issued together branch-free, 4 early exit past the last row
 #endif
+#ifndef WSG_FAN_KSEL
+#define WSG_FAN_KSEL 2   // fan-out period path: a pass's keys by ds_bpermute one pass ahead (2: C4 8.32 vs 8.40 us), in the pass (0), v_readlane + per-lane select (1: 8.6 us)
+#endif
 #ifndef WSG_FAN_UNROLL
 #define WSG_FAN_UNROLL 1   // fan-out period path: passes per loop iteration (A/B)
 #endif
@@ -1649,11 +1652,11 @@ __device__ __forceinline__ void fan_tm_finish(const FanWin& w, const FanGeom& f,
 }
 
 template <int P>
-__global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict__ payload0, uint64_t len,
+__global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restrict__ payload0, uint64_t len,
                                                       const uint32_t* __restrict__ keys, uint32_t k, uint8_t opcode,
                                                       uint32_t mask, uint64_t fsize, uint32_t G, uint32_t dm,
                                                       uint8_t* __restrict__ wire0, const FanMsgs msgs, v4u hp0,
-                                                      uint32_t nwaves)
+                                                      uint32_t nwaves, uint32_t wpb)
 {
     constexpr int KW = 2 * P;   // keys per pass: the row spans <= 2 groups (G >= 64)
     if (WSG_DIAG_FAN & 256)     // diagnostic: the launch of the grid alone
@@ -1665,7 +1668,7 @@ __global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict_
     // asm consumes them all, so they are issued together and waited once
     if (WSG_FAN_PRO & 1)
         asm volatile("" ::"s"(payload0), "s"(len), "s"(keys), "s"(k), "s"(fsize), "s"(G), "s"(dm), "s"(wire0),
-                     "s"(nwaves), "s"(src_off), "s"(dst_off), "s"(uint32_t(opcode)), "s"(mask));
+                     "s"(nwaves), "s"(wpb), "s"(src_off), "s"(dst_off), "s"(uint32_t(opcode)), "s"(mask));
     const uint8_t* __restrict__ payload = payload0 + src_off;
     uint8_t* __restrict__ wire = wire0 + dst_off;
     FanGeom f;   // fan_geom() with the header bytes from the host (hp0)
@@ -1681,7 +1684,10 @@ __global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict_
     // gridDim: the dispatch packet is one more memory read before the first
     // store); rows are wave-uniform, so the write-through stores' buffer
     // resource sits in SGPRs (else every store becomes a waterfall loop)
-    const uint64_t row0 = uint64_t(blockIdx.x) * 64;
+    const uint32_t wid = blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave of W
+    if (wid >= nwaves)   // the last workgroup's spare waves
+        return;
+    const uint64_t row0 = uint64_t(wid) * 64;
     const uint64_t rstep = uint64_t(nwaves) * 64;   // W rows: a multiple of G (dm groups)
     if ((WSG_FAN_PRO & 4) && row0 >= chunks)   // a wave past the last row (its loads are guarded anyway)
         return;
@@ -1757,6 +1763,21 @@ __global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict_
             st16nt(wire + (row0 + lane) * CHUNK, w);
         return;
     }
+    // WSG_FAN_KSEL 2: the next pass's two shuffles are issued before this
+    // pass's stores, so their LDS latency is off the loop's critical path
+    auto pass_keys = [&](uint32_t it, uint32_t& ka, uint32_t& kb) {
+        const uint32_t slot = it * KW;
+        uint32_t kreg = kv[0];
+#pragma unroll
+        for (int h = 1; h < WSG_FAN_KV; ++h)
+            kreg = (slot >> 6) == uint32_t(h) ? kv[h] : kreg;
+        const uint32_t sb = (slot & 63) * 4;
+        ka = __builtin_amdgcn_ds_bpermute(int(addr + sb), int(kreg));
+        kb = __builtin_amdgcn_ds_bpermute(int(addr + sb + 4), int(kreg));
+    };
+    uint32_t ka_next = 0, kb_next = 0;
+    if (WSG_FAN_KSEL == 2)
+        pass_keys(0, ka_next, kb_next);
 #pragma unroll WSG_FAN_UNROLL
     for (uint32_t it = 0; row < chunks; ++it) {
         const uint32_t slot = it * KW;                      // wave-uniform; KW divides 64
@@ -1764,9 +1785,32 @@ __global__ __launch_bounds__(64) void k_fanout_period(const uint8_t* __restrict_
 #pragma unroll
         for (int h = 1; h < WSG_FAN_KV; ++h)
             kreg = (slot >> 6) == uint32_t(h) ? kv[h] : kreg;
-        const uint32_t sb = (slot & 63) * 4;
-        const uint32_t ka = __builtin_amdgcn_ds_bpermute(int(addr + sb), int(kreg));
-        const uint32_t kb = __builtin_amdgcn_ds_bpermute(int(addr + sb + 4), int(kreg));
+        uint32_t ka, kb;
+        if (WSG_FAN_KSEL == 2) {
+            ka = ka_next;
+            kb = kb_next;
+            pass_keys(it + 1, ka_next, kb_next);   // (past the last pass: slots of kv, unused)
+        } else if (WSG_FAN_KSEL) {
+            // the pass's KW keys read into SGPRs (v_readlane: no LDS round
+            // trip in the loop's dependency chain), each lane picking its
+            // two by its fixed slot ia (the compares are loop-invariant)
+            const uint32_t base = slot & 63;
+            uint32_t kq[KW + 1];
+#pragma unroll
+            for (int q = 0; q <= KW; ++q)
+                kq[q] = __builtin_amdgcn_readlane(kreg, (base + uint32_t(q)) & 63u);   // kq[KW]: only for ia = KW - 1, unused
+            ka = kq[0];
+            kb = kq[1];
+#pragma unroll
+            for (int q = 1; q < KW; ++q) {
+                ka = ia == uint32_t(q) ? kq[q] : ka;
+                kb = ia == uint32_t(q) ? kq[q + 1] : kb;
+            }
+        } else {
+            const uint32_t sb = (slot & 63) * 4;
+            ka = __builtin_amdgcn_ds_bpermute(int(addr + sb), int(kreg));
+            kb = __builtin_amdgcn_ds_bpermute(int(addr + sb + 4), int(kreg));
+        }
         const uint32_t ra = __builtin_amdgcn_alignbit(ka, ka, sa), rb = __builtin_amdgcn_alignbit(kb, kb, sbr);
         const v4u w = t ^ (ma & v4u{ra, ra, ra, ra}) ^ (mb & v4u{rb, rb, rb, rb});
         if ((WSG_DIAG_FAN & 64) && (w[0] & w[1] & w[2] & w[3]) != 0xA5C3E1F7u) {
@@ -1892,7 +1936,7 @@ hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64
 // to leave the batch to k_fanout_flat.  Wave count W = Q * s with W * 64 a
 // multiple of G (Q = G / gcd(G, 64)), about `waves` of them, and few enough
 // passes per wave that one key load covers them (passes * 2P <= 64 * WSG_FAN_KV).
-bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_t* payload, uint64_t len,
+bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, int wpb, const uint8_t* payload, uint64_t len,
                           const uint32_t* keys, uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize,
                           uint8_t* wire, const FanMsgs& msgs, uint32_t nmsgs, hipError_t* err)
 {
@@ -1923,7 +1967,11 @@ bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_
     if (W > (1u << 22))
         return false;
     const uint32_t dm = uint32_t(W * 64 / G);
-    // waves per block: one (4-wave blocks measured 8 % slower at C4)
+    // workgroups of wpb waves (the last one's spare waves return at once):
+    // dispatching one-wave workgroups was most of a C4 launch
+    if (wpb < 1 || wpb > 16)
+        wpb = 1;
+    const uint32_t blocks = uint32_t((W + uint64_t(wpb) - 1) / uint64_t(wpb));
     // header bytes before the key (<= 10), the same in every frame
     const SendGeom sg = send_geom(opcode, mask != 0, len, 0);
     const uint32_t kpos = sg.hdr - (mask ? 4u : 0u);
@@ -1933,16 +1981,19 @@ bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, const uint8_
     const v4u hp0 = v4u{hw[0], hw[1], hw[2], hw[3]};
     switch (P) {
     case 1:
-        k_fanout_period<1><<<dim3(uint32_t(W), nmsgs), 64, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm,
-                                                               wire, msgs, hp0, uint32_t(W));
+        k_fanout_period<1><<<dim3(blocks, nmsgs), 64 * uint32_t(wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize,
+                                                                             uint32_t(G), dm, wire, msgs, hp0, uint32_t(W),
+                                                                             uint32_t(wpb));
         break;
     case 2:
-        k_fanout_period<2><<<dim3(uint32_t(W), nmsgs), 64, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm,
-                                                               wire, msgs, hp0, uint32_t(W));
+        k_fanout_period<2><<<dim3(blocks, nmsgs), 64 * uint32_t(wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize,
+                                                                             uint32_t(G), dm, wire, msgs, hp0, uint32_t(W),
+                                                                             uint32_t(wpb));
         break;
     default:
-        k_fanout_period<4><<<dim3(uint32_t(W), nmsgs), 64, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, uint32_t(G), dm,
-                                                               wire, msgs, hp0, uint32_t(W));
+        k_fanout_period<4><<<dim3(blocks, nmsgs), 64 * uint32_t(wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize,
+                                                                             uint32_t(G), dm, wire, msgs, hp0, uint32_t(W),
+                                                                             uint32_t(wpb));
         break;
     }
     *err = hipGetLastError();

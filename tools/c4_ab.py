@@ -1,6 +1,8 @@
 """C4 fan-out variants timed as bench.py times its c4 leg: one prepared
 wsg_fanout_encode per step, HIP events around a region of K back-to-back
-launches (no events between launches), interleaved over variants.
+launches (no events between launches), interleaved over variants; by default the K
+launches are one captured graph, replayed ($GRAPH=0: launched from Python,
+where the host's ~6-7 us per call can bound a short kernel).
 
 usage: python tools/c4_ab.py [NAME=VALUE@]path/to/libwsg.so ...   ($K, $REPS)
 (NAME=VALUE is set in the environment before that library's context is made;
@@ -39,21 +41,37 @@ def main():
     kt = torch.from_numpy(keys.view(np.int32)).cuda()
     ref = None
     launches, wires = [], []
+    graph = os.environ.get("GRAPH", "1") == "1"
     for s in specs:
         c = make_codec(s)
         w = torch.empty(fsz * len(keys), dtype=torch.uint8, device="cuda")
-        launches.append(c.prepare_fanout(p, kt, 0x82, True, w))
+        launch = c.prepare_fanout(p, kt, 0x82, True, w)
+        if graph:
+            # K launches captured once and replayed: the host's cost per
+            # launch (a ctypes call, ~6-7 us) no longer bounds the region
+            launch()
+            torch.cuda.synchronize()
+            st = torch.cuda.Stream()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(st):
+                launch()   # warm on the capture stream
+                st.synchronize()
+                with torch.cuda.graph(g, stream=st):
+                    for _ in range(k):
+                        launch()
+            launch = g.replay
+        launches.append(launch)
         wires.append(w)
     alg = len(payload) + 4 * len(keys) + fsz * len(keys)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     res = [[] for _ in specs]
     for _ in range(int(os.environ.get("REPS", 7))):
         for i, launch in enumerate(launches):
-            for _ in range(50):
+            for _ in range(1 if graph else 50):
                 launch()
             torch.cuda.synchronize()
             e0.record()
-            for _ in range(k):
+            for _ in range(1 if graph else k):
                 launch()
             e1.record()
             e1.synchronize()
