@@ -75,7 +75,7 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #define WSG_FAN_PRO 1   // fan-out period path prologue (A/B, tools/c4_ab.py): 1 all kernel arguments loaded in one round, 2 both payload windows issued together branch-free, 4 early exit past the last row
 #endif
 #ifndef WSG_FAN_KSEL
-#define WSG_FAN_KSEL 2   // fan-out period path: a pass's keys by ds_bpermute one pass ahead (2: C4 8.32 vs 8.40 us), in the pass (0), v_readlane + per-lane select (1: 8.6 us)
+#define WSG_FAN_KSEL 2   // fan-out period path: a pass's keys by ds_bpermute one pass ahead (2: C4 8.32 vs 8.40 us) or in the pass (0); v_readlane + per-lane selects measured 8.6 us (round 3)
 #endif
 #ifndef WSG_FAN_UNROLL
 #define WSG_FAN_UNROLL 1   // fan-out period path: passes per loop iteration (A/B)
@@ -1753,82 +1753,85 @@ __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restric
     // rows, so a pass is ~2 shuffles, ~12 VALU and one 1 KiB store.
     const uint32_t sa = 8u * (pa & 3u), sbr = 8u * (pb & 3u);
     const uint64_t full_rows_end = chunks & ~uint64_t(63);   // rows below this are whole (64 chunks)
-    uint64_t row = row0;
-    uint8_t* wrow = wire + row0 * CHUNK;
+    // this wave's passes (rows row0 + it * rstep below chunks), the first
+    // n_full of them whole rows: 32-bit scalar loop counters instead of
+    // 64-bit row compares in the loop
+    const uint32_t n_pass = row0 < chunks ? uint32_t((chunks - row0 + rstep - 1) / rstep) : 0u;
+    const uint32_t n_full = row0 < full_rows_end ? uint32_t((full_rows_end - row0 + rstep - 1) / rstep) : 0u;
     const uint64_t wstep = rstep * CHUNK;
-    uint32_t addr = ia * 4;                                 // shuffle address of key slot ia of pass 0
+    const uint32_t addr = ia * 4;                           // shuffle address of key slot ia of pass 0
     if (WSG_DIAG_FAN & 128) {   // diagnostic: the prologue alone (its results kept live)
         const v4u w = t ^ ma ^ mb ^ v4u{kv[0], kv[WSG_FAN_KV - 1], addr, 0};
         if ((w[0] & w[1] & w[2] & w[3]) == 0xA5C3E1F7u && row0 + lane < chunks)
             st16nt(wire + (row0 + lane) * CHUNK, w);
         return;
     }
-    // WSG_FAN_KSEL 2: the next pass's two shuffles are issued before this
-    // pass's stores, so their LDS latency is off the loop's critical path
-    auto pass_keys = [&](uint32_t it, uint32_t& ka, uint32_t& kb) {
-        const uint32_t slot = it * KW;
+    // The keys of pass `it` for this lane: frame a's (slot ia) and, where a
+    // frame starts inside the lane's chunk, frame b's (slot ia + 1).
+    auto pass_keys = [&](uint32_t it, uint32_t& ka, uint32_t& kb, bool want_b) {
+        const uint32_t slot = it * KW;                      // wave-uniform; KW divides 64
         uint32_t kreg = kv[0];
 #pragma unroll
         for (int h = 1; h < WSG_FAN_KV; ++h)
             kreg = (slot >> 6) == uint32_t(h) ? kv[h] : kreg;
         const uint32_t sb = (slot & 63) * 4;
         ka = __builtin_amdgcn_ds_bpermute(int(addr + sb), int(kreg));
-        kb = __builtin_amdgcn_ds_bpermute(int(addr + sb + 4), int(kreg));
+        kb = want_b ? __builtin_amdgcn_ds_bpermute(int(addr + sb + 4), int(kreg)) : 0u;
     };
-    uint32_t ka_next = 0, kb_next = 0;
-    if (WSG_FAN_KSEL == 2)
-        pass_keys(0, ka_next, kb_next);
-#pragma unroll WSG_FAN_UNROLL
-    for (uint32_t it = 0; row < chunks; ++it) {
-        const uint32_t slot = it * KW;                      // wave-uniform; KW divides 64
-        uint32_t kreg = kv[0];
-#pragma unroll
-        for (int h = 1; h < WSG_FAN_KV; ++h)
-            kreg = (slot >> 6) == uint32_t(h) ? kv[h] : kreg;
-        uint32_t ka, kb;
-        if (WSG_FAN_KSEL == 2) {
-            ka = ka_next;
-            kb = kb_next;
-            pass_keys(it + 1, ka_next, kb_next);   // (past the last pass: slots of kv, unused)
-        } else if (WSG_FAN_KSEL) {
-            // the pass's KW keys read into SGPRs (v_readlane: no LDS round
-            // trip in the loop's dependency chain), each lane picking its
-            // two by its fixed slot ia (the compares are loop-invariant)
-            const uint32_t base = slot & 63;
-            uint32_t kq[KW + 1];
-#pragma unroll
-            for (int q = 0; q <= KW; ++q)
-                kq[q] = __builtin_amdgcn_readlane(kreg, (base + uint32_t(q)) & 63u);   // kq[KW]: only for ia = KW - 1, unused
-            ka = kq[0];
-            kb = kq[1];
-#pragma unroll
-            for (int q = 1; q < KW; ++q) {
-                ka = ia == uint32_t(q) ? kq[q] : ka;
-                kb = ia == uint32_t(q) ? kq[q + 1] : kb;
+    // The pass loop, in two forms: a frame starts inside a chunk at only
+    // ~P positions of a group's G, so most waves hold no such lane (mb = 0
+    // in every lane, fixed for all passes) and skip frame b's key and
+    // masking; the loop is VALU-bound once the shuffles are off its chain.
+    auto passes = [&](auto has_b) {
+        constexpr bool B = decltype(has_b)::value;
+        uint32_t ka_n = 0, kb_n = 0;
+        if (WSG_FAN_KSEL == 2)
+            pass_keys(0, ka_n, kb_n, B);
+        auto word = [&](uint32_t it) {
+            uint32_t ka, kb;
+            if (WSG_FAN_KSEL == 2) {
+                // this pass's keys were shuffled during the previous pass;
+                // the next pass's go out now, ahead of this pass's store
+                ka = ka_n;
+                kb = kb_n;
+                pass_keys(it + 1, ka_n, kb_n, B);   // (past the last pass: slots of kv, unused)
+            } else {
+                pass_keys(it, ka, kb, B);
             }
-        } else {
-            const uint32_t sb = (slot & 63) * 4;
-            ka = __builtin_amdgcn_ds_bpermute(int(addr + sb), int(kreg));
-            kb = __builtin_amdgcn_ds_bpermute(int(addr + sb + 4), int(kreg));
-        }
-        const uint32_t ra = __builtin_amdgcn_alignbit(ka, ka, sa), rb = __builtin_amdgcn_alignbit(kb, kb, sbr);
-        const v4u w = t ^ (ma & v4u{ra, ra, ra, ra}) ^ (mb & v4u{rb, rb, rb, rb});
-        if ((WSG_DIAG_FAN & 64) && (w[0] & w[1] & w[2] & w[3]) != 0xA5C3E1F7u) {
-            // diagnostic: the computation without its stores
-        } else if (row < full_rows_end) {
-            // a whole row: one 16-B store per lane
-            if (WSG_FAN_SC1) {
+            const uint32_t ra = __builtin_amdgcn_alignbit(ka, ka, sa);
+            v4u w = t ^ (ma & v4u{ra, ra, ra, ra});
+            if constexpr (B) {
+                const uint32_t rb = __builtin_amdgcn_alignbit(kb, kb, sbr);
+                w ^= mb & v4u{rb, rb, rb, rb};
+            }
+            return w;
+        };
+        uint8_t* wrow = wire + row0 * CHUNK;
+#pragma unroll WSG_FAN_UNROLL
+        for (uint32_t it = 0; it < n_full; ++it) {
+            const v4u w = word(it);
+            if ((WSG_DIAG_FAN & 64) && (w[0] & w[1] & w[2] & w[3]) != 0xA5C3E1F7u) {
+                // diagnostic: the computation without its stores
+            } else if (WSG_FAN_SC1) {
                 const OutTile ot(wrow, 64 * CHUNK, true);   // write-through (resource at the row)
                 ot.put(lane * CHUNK, w);
             } else {
                 st16nt(wrow + lane * CHUNK, w);
             }
-        } else if (row + lane < chunks) {
-            fan_store(wire, row + lane, chunks, total, w);   // the last, partial row
+            wrow += wstep;
         }
-        row += rstep;
-        wrow += wstep;
-    }
+        if (n_pass > n_full) {   // the last, partial row (the job's final row only)
+            const uint64_t row = row0 + uint64_t(n_full) * rstep;
+            const v4u w = word(n_full);
+            if (row + lane < chunks)
+                fan_store(wire, row + lane, chunks, total, w);
+        }
+    };
+    const bool any_b = __ballot((mb[0] | mb[1] | mb[2] | mb[3]) != 0u) != 0;   // wave-uniform
+    if (any_b)
+        passes(std::true_type{});
+    else
+        passes(std::false_type{});
 }
 
 // Single-buffer XOR used by the per-frame host path: dst[i] = src[i] ^
