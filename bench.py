@@ -943,6 +943,37 @@ def fanout_many_leg(w, m=16, reps=10):
             "write_GBps": round(bytes_out / (ms * 1e-3) / 1e9, 1), "frame_bytes": fsz}
 
 
+def c4_graph_leg(w, steps, reps=5):
+    """C4 as a captured graph of `steps` fan-out launches, replayed `reps`
+    times; HIP events around each replay.  Per-launch time and its frac."""
+    import statistics
+
+    t = w.torch
+    st = t.cuda.Stream()
+    g = t.cuda.CUDAGraph()
+    with t.cuda.stream(st):
+        w.launch()   # warm on the capture stream
+        st.synchronize()
+        with t.cuda.graph(g, stream=st):
+            for _ in range(steps):
+                w.launch()
+    g.replay()
+    t.cuda.synchronize()
+    e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+    us = []
+    for _ in range(reps):
+        e0.record()
+        g.replay()
+        e1.record()
+        e1.synchronize()
+        us.append(e0.elapsed_time(e1) * 1e3 / steps)
+    med = statistics.median(us)
+    return {"launches_per_replay": steps, "replays": reps, "us_per_launch": round(med, 3),
+            "achieved_GBps": round(w.alg_bytes / (med * 1e-6) / 1e9, 1),
+            "frac": round(w.alg_bytes / (med * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+            "value_GiBps": round(w.payload_bytes / (med * 1e-6) / GIB, 2)}
+
+
 def roofline_obj(kernel, alg_bytes, avg_ms, traffic, timing, minmax=None):
     """The roofline object of one kernel: algorithmic bytes per launch over
     its average launch duration (HIP events on its launch stream), against
@@ -1091,6 +1122,11 @@ def config_obj(args, cfg, codec, rank, world, device, steps, warmup, cpu):
         if cfg == "c3":
             obj["k_decode_per_launch"] = decode_launches(w)
         if cfg == "c4":
+            # C4 is launch-latency sensitive, report it with a graph
+            # of repeats too: the same prepared launch captured `steps` times
+            # and replayed once (a Python call per launch costs ~6-7 us, close
+            # to the 8 us kernel, and can bound the eager region on a slow host)
+            obj["graph_replay"] = c4_graph_leg(w, steps)
             # the ws_multicast tick's form: 16 such messages in ONE launch
             # (wsg_fanout_encode_many), where one 41 MB fan-out is too short
             # to reach the write rate on its own
