@@ -71,6 +71,9 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_FAN_PERIOD
 #define WSG_FAN_PERIOD 1   // fan-out: period path (k_fanout_period) where the frame size allows; 0 = flat kernel only
 #endif
+#ifndef WSG_ENC_PRO
+#define WSG_ENC_PRO 0   // k_encode_mask: 1 = the prologue's independent loads in one round (A/B, tools/tune_enc.py: C3 -0.5 %, C5 share +2 %; not kept)
+#endif
 #ifndef WSG_FAN_PRO
 #define WSG_FAN_PRO 1   // fan-out period path prologue (A/B, tools/c4_ab.py): 1 all kernel arguments loaded in one round, 2 both payload windows issued together branch-free, 4 early exit past the last row
 #endif
@@ -1119,11 +1122,35 @@ __global__ __launch_bounds__(BLOCK) void k_encode_mask(const uint8_t* __restrict
                                                        uint8_t* __restrict__ wire, uint64_t wire_cap,
                                                        uint32_t q_begin, uint32_t q_end)
 {
-    if (wire_off[n] > wire_cap)
-        return;   // capacity error latched by k_encode_finalize
-    // this launch's pieces: [q_begin, min(all pieces, q_end))
-    const uint32_t pieces = min(piece_start[n], q_end);
     const uint32_t waves = gridDim.x * (BLOCK / 64);
+    uint32_t q = q_begin + blockIdx.x * (BLOCK / 64) + wave_id();
+    uint32_t pieces, f_first = 0, f_second = 0;
+    if (WSG_ENC_PRO) {
+        // The prologue's independent loads in one round: the batch's end and
+        // piece count, and this wave's first two piece -> frame entries (the
+        // map holds q_end entries; entries past the batch's pieces are never
+        // used).  Left to the compiler these came in seven dependent scalar
+        // rounds (kernel arguments among them) before a piece's first data
+        // load, several us per wave for 4 KiB of work.
+        // (no asm barrier before these loads: the compiler then treats
+        // memory as possibly written and turns them into vector loads)
+        const uint64_t end = wire_off[n];
+        const uint32_t pall = piece_start[n];
+        f_first = piece_frame[min(q, q_end - 1)];           // (clamped, not branched: one round)
+        f_second = piece_frame[min(q + waves, q_end - 1)];
+        // identity asm (no memory effect): the four values exist here, so
+        // the compiler cannot sink their loads past the exits below
+        uint64_t e = end;
+        uint32_t pa = pall;
+        asm("" : "+s"(e), "+s"(pa), "+s"(f_first), "+s"(f_second));
+        if (e > wire_cap)
+            return;   // capacity error latched by k_encode_finalize
+        pieces = min(pa, q_end);     // this launch's pieces: [q_begin, min(all pieces, q_end))
+    } else {
+        if (wire_off[n] > wire_cap)
+            return;   // capacity error latched by k_encode_finalize
+        pieces = min(piece_start[n], q_end);
+    }
     // Software pipeline over the wave's pieces: while piece q streams, the
     // descriptor of piece q + W (frame index already known) and the frame
     // index of piece q + 2W are in flight, so the dependent metadata loads
@@ -1134,11 +1161,10 @@ __global__ __launch_bounds__(BLOCK) void k_encode_mask(const uint8_t* __restrict
         uint32_t ps;
     };
     auto meta = [&](uint32_t i) { return Meta{load_desc(desc + i), wire_off[i], piece_start[i]}; };
-    uint32_t q = q_begin + blockIdx.x * (BLOCK / 64) + wave_id();
     if (q >= pieces)
         return;
-    Meta cur = meta(piece_frame[q]);
-    uint32_t i_next = (q + waves < pieces) ? piece_frame[q + waves] : 0;
+    Meta cur = meta(WSG_ENC_PRO ? f_first : piece_frame[q]);
+    uint32_t i_next = (q + waves < pieces) ? (WSG_ENC_PRO ? f_second : piece_frame[q + waves]) : 0;
     for (;;) {
         Piece<WSG_ENC_NT_SRC != 0> pc;
         pc.load(make_rec(cur.off, payload + cur.d.src_off, cur.d.len, cur.d.key, cur.d.status, cur.d.opcode,
