@@ -146,8 +146,10 @@ def main():
                 break
         cases.append(run_case(world, 4000, 300, root=world - 1, seed=11 + world))
     cases.append(run_case(3, 3000, 500, root=0, bad=1, seed=17))
-    if big:   # C5-shape frames at world 2: 64 Ki frames x 16 KiB (1 GiB of payload)
+    if big:   # C5-shape frames at world 2: 64 Ki frames x 16 KiB (1 GiB of payload); world 4
         cases.append(run_case(2, 65536, 1024, seed=-1, timeout=240))
+        cases.append(run_case(4, 9000, 1024, root=3, seed=4 * 7919 + 10024))
+        cases.append(run_case(4, 5000, 700, root=0, bad=2, seed=23))
     print(json.dumps(dict(cases=cases)), flush=True)
 
 
