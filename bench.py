@@ -783,13 +783,112 @@ def gather_leg(w, world, rank, device):
     return res
 
 
+def c5_rank_leg(world, rank, local, device, n_total=1 << 20, size=16384, chunk=1024, reps=3):
+    """BASELINE config C5 beside the weak-scaling headline at N > 1, through
+    the product's own multi-GPU entry in its one-process-per-GPU form (SURVEY
+    §8b-3 / §8e): every torchrun rank joins a wsg_mgpu group
+    (wsg_mgpu_create_rank; rank 0's wsg_mgpu_unique_id handed out over the
+    host group) and calls wsg_mgpu_encode_gather on its round-robin shard of
+    the 1 Mi x 16 KiB job (1024-frame chunks, payloads made in HBM): its GPU
+    encodes the shard, then the library's grouped ncclSend / ncclRecv move
+    every chunk straight to its place in rank 0's output (RCCL over xGMI),
+    and k_rebase_offsets writes the job's frame offsets there.
+
+    Per rank: the encode (HIP events on the group context's stream around
+    wsg_encode_batch, and around k_encode_mask alone for the roofline) and
+    the gather (events on the stream the transfers run on), each the max
+    over ranks; root ingress GB/s beside SURVEY §8e's ~1.07 TB/s (7 xGMI
+    links); the root's output against the oracle (sampled frames) and its
+    offsets against the closed form."""
+    import torch
+    import torch.distributed as dist
+
+    import cppserver_amd as ca
+    from cppserver_amd import shard
+    from cppserver_amd import workloads as wl
+
+    group = CPU_GROUP if CPU_GROUP is not None else dist.group.WORLD
+    obj = [ca.MultiGPU.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    g = ca.MultiGPU.rank(local, obj[0], rank, world)
+    try:
+        ids = shard.rank_frames(rank, world, n_total, chunk)
+        payload = wl.c5_payload_torch(ids, size, device=device)
+        desc = ca.desc_to_tensor(wl.c5_desc(ids, size), device)
+        fsz = ca.frame_size(0x82, True, size)
+        n_local = len(ids)
+        wire = torch.empty(max(n_local * fsz, 16), dtype=torch.uint8, device=device)
+        woff = torch.empty(n_local + 1, dtype=torch.int64, device=device)
+        out = out_off = None
+        if rank == 0:
+            out = torch.empty(n_total * fsz, dtype=torch.uint8, device=device)
+            out_off = torch.empty(n_total + 1, dtype=torch.int64, device=device)
+        torch.cuda.synchronize()
+
+        def call():
+            return g.encode_gather(n_total, chunk, [payload], [desc], [wire], [woff], root=0, out=out,
+                                   out_off=out_off)
+
+        call()   # warm: RCCL connections, the library's scratch
+        g.timing(True, every=1)
+        g.timing_read(reset=True)
+        enc, gat, wall = [], [], []
+        for _ in range(reps):
+            dist.barrier(group=group)
+            t0 = time.perf_counter()
+            e_ms, g_ms = call()
+            wall.append((time.perf_counter() - t0) * 1e3)
+            enc.append(e_ms)
+            gat.append(g_ms)
+        k_ms, k_n = g.timing_read(reset=True)
+        g.timing(False)
+        k_avg = k_ms / max(k_n, 1)
+        enc_ms = max_over_ranks(min(enc), world, device)
+        gat_ms = max_over_ranks(min(gat), world, device)
+        wall_ms = max_over_ranks(min(wall), world, device)
+        k_max = max_over_ranks(k_avg, world, device)
+        k_min = -max_over_ranks(-k_avg, world, device)
+        alg = n_local * (size + fsz)   # k_encode_mask: read payload + write frames (this rank)
+        res = {"workload": "C5: %d x %d B frames round-robin (chunks of %d) over %d GPUs, gather to rank 0"
+                           % (n_total, size, chunk, world),
+               "path": "C-ABI rank form: wsg_mgpu_create_rank + wsg_mgpu_encode_gather (RCCL grouped send/recv)",
+               "calls": reps, "encode_ms": round(enc_ms, 4),
+               "encode_GiBps_job": round(n_total * size / (enc_ms * 1e-3) / GIB, 1),
+               "gather_ms": round(gat_ms, 3), "wall_ms": round(wall_ms, 3),
+               "roofline_per_rank": roofline_obj("k_encode_mask", alg, k_max, None,
+                                                 "HIP events around k_encode_mask on each rank's group stream, "
+                                                 "best of %d calls' average; slowest rank" % reps),
+               "k_encode_mask_ms_fastest_rank": round(k_min, 5)}
+        if rank == 0:
+            moved = n_total * fsz - n_local * fsz
+            res.update({"bytes_into_root": moved, "GBps_into_root": round(moved / (gat_ms * 1e-3) / 1e9, 1),
+                        "root_ingress_expectation_GBps": 1071 if world == 8 else None,
+                        "job_bytes": n_total * fsz})
+            ok = bool(torch.equal(out_off, torch.arange(n_total + 1, dtype=torch.int64, device=device) * fsz))
+            import oracle
+
+            for q in sorted({0, 1, chunk - 1, chunk, chunk * (world - 1) + 5, n_total // 2 + 3, n_total - 1}):
+                if q >= n_total:
+                    continue
+                d = wl.c5_desc(np.array([q]), size)
+                d["src_off"] = 0
+                ref, _ = oracle.encode_batch(wl.c5_payload_np(np.array([q]), size), d)
+                ok &= bool(np.array_equal(out[q * fsz: (q + 1) * fsz].cpu().numpy(), ref))
+            res["root_check"] = bool(ok)
+        del payload, wire, out
+        torch.cuda.empty_cache()
+        return res
+    finally:
+        g.close()
+
+
 def c5_job_leg(world, rank, device, codec, n_total=1 << 20, size=16384, chunk=1024):
-    """BASELINE config C5 beside the weak-scaling headline at N > 1: the 1 Mi x
-    16 KiB job dealt round-robin over the ranks (1024-frame chunks), every
-    rank encodes its shard on its GPU (wsg_encode_batch, payloads made in HBM),
-    and the framed output goes to rank 0 over RCCL (torch.distributed's
-    group); rank 0 reassembles the job in frame order and checks sampled
-    frames against the oracle.  Encode and gather times are max over ranks."""
+    """Cross-check of c5_rank_leg through torch.distributed instead of the
+    product's entry: the same round-robin shards encoded per rank
+    (wsg_encode_batch), the framed output moved to rank 0 by torch's RCCL
+    group (cppserver_amd.shard.gather_frames), reassembled in frame order
+    and sampled against the oracle.  Encode and gather times are max over
+    ranks."""
     import torch
 
     import cppserver_amd as ca
@@ -1191,8 +1290,33 @@ def warm_up(w, min_steps, seconds):
     return done
 
 
+CHECK_KEYS = ("spot_check", "root_check", "check", "payload_ok", "delivered_ok", "roundtrip_ok", "all_delivered",
+              "wire_ok", "off_ok")
+
+
+def failed_checks(obj, path=""):
+    """Every parity / delivery check in the line's legs that is false, and
+    every leg that recorded an error, as dotted paths (the run exits non-zero
+    when there is any)."""
+    out = []
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            p = path + "." + k if path else k
+            if k in CHECK_KEYS and v is not True:
+                out.append("%s=%s" % (p, v))
+            elif k == "error":
+                out.append("%s: %s" % (path or k, str(v)[:120]))
+            else:
+                out.extend(failed_checks(v, p))
+    elif isinstance(obj, list):
+        for i, v in enumerate(obj):
+            out.extend(failed_checks(v, "%s[%d]" % (path, i)))
+    return out
+
+
 def main():
     args = parse()
+    failed = []
     import torch
 
     import cppserver_amd as ca
@@ -1239,17 +1363,27 @@ def main():
         except Exception as e:   # noqa: BLE001  (reported; the headline stands)
             extras["pcie_inclusive_all_ranks"] = {"error": repr(e)[:300]}
     if w.cfg == "c2" and world > 1 and not args.no_c5_job:
-        # C5 (BASELINE configs[4]) on the same GPUs: a failure here is reported
-        # in the line, it does not take the headline with it
+        # C5 (BASELINE configs[4]) on the same GPUs through the product's RCCL
+        # rank form; a failure is reported in the line (and fails the run, see
+        # failed_checks), it does not take the headline's numbers with it
+        c5_frames = int(os.environ.get("WSG_C5_FRAMES", 1 << 20))
         try:
-            extras["c5_job"] = c5_job_leg(world, rank, device, codec,
-                                          n_total=int(os.environ.get("WSG_C5_FRAMES", 1 << 20)))
+            extras["c5_job"] = c5_rank_leg(world, rank, local, device, n_total=c5_frames)
         except Exception as e:   # noqa: BLE001
             extras["c5_job"] = {"error": repr(e)[:300]}
+        torch.cuda.empty_cache()
+        if os.environ.get("WSG_BENCH_TORCH_GATHER", "1") != "0":
+            # labelled cross-check: the same job gathered by torch.distributed
+            try:
+                extras["c5_job_torch_crosscheck"] = c5_job_leg(world, rank, device, codec, n_total=c5_frames)
+            except Exception as e:   # noqa: BLE001
+                extras["c5_job_torch_crosscheck"] = {"error": repr(e)[:300]}
         if os.environ.get("WSG_BENCH_CAPI_RCCL", "1") != "0":
-            capi = c5_capi_leg(world, rank, n_total=int(os.environ.get("WSG_C5_FRAMES", 1 << 20)))
+            # the one-process form of the same entry (wsg_mgpu_create over all
+            # N GPUs, device / xGMI peer copies), in a child process
+            capi = c5_capi_leg(world, rank, n_total=c5_frames)
             if capi is not None:
-                extras["c5_job_capi"] = capi
+                extras["c5_job_one_process"] = capi
     cpu = host_cpu() if (rank == 0 and world == 1 and not args.no_cpu) else None
     cpu1 = cpu_mt = None
     if cpu is not None:
@@ -1326,12 +1460,25 @@ def main():
             "spot_check": ok,
         }
         line.update(extras)
+        failed = failed_checks(extras)
+        if not ok:
+            failed.insert(0, "spot_check (headline)")
+        # the top-level spot_check is every leg's parity check and root check
+        # together; the headline's own stays beside it
+        line["spot_check_headline"] = ok
+        line["spot_check"] = not failed
+        line["failed_checks"] = failed
         print(json.dumps(line), flush=True)
+        if failed:
+            print("bench.py: %d failed check(s) or leg error(s): %s" % (len(failed), "; ".join(failed)),
+                  file=sys.stderr, flush=True)
     if world > 1:
         import torch.distributed as dist
 
         dist.destroy_process_group()
     codec.close()
+    if rank == 0 and failed:
+        sys.exit(1)
 
 
 if __name__ == "__main__":

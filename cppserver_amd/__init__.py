@@ -19,7 +19,9 @@ from .layout import (  # noqa: F401  (re-exported)
 )
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libwsg.so")
+# $WSG_LIB_PATH: another build of the same ABI for a one-off A/B check (tools/);
+# unset, the in-tree library
+LIB_PATH = os.environ.get("WSG_LIB_PATH") or os.path.join(_HERE, "_build", "libwsg.so")
 ROOT = os.path.dirname(_HERE)
 HEADERS = [os.path.join(ROOT, "include", "wsg_capi.h")]
 
@@ -664,6 +666,23 @@ class MultiGPU:
             self._g = None
 
     __del__ = close
+
+    def _ctx(self, i):
+        ctx = self._L.wsg_mgpu_ctx(self._g, int(i))
+        if not ctx:
+            raise WSGError(WSG_EINVAL, "wsg_mgpu_ctx(%d)" % i)
+        return ctypes.c_void_p(ctx)
+
+    def timing(self, on=True, every=1, i=0):
+        """Time the dominant kernel of local rank i's encodes (its context's
+        HIP events, as Codec.timing): k_encode_mask inside encode_gather."""
+        _check(self._L.wsg_timing_enable(self._ctx(i), int(every) if on else 0), "wsg_timing_enable")
+
+    def timing_read(self, reset=True, i=0):
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        _check(self._L.wsg_timing_read(self._ctx(i), ctypes.byref(ms), ctypes.byref(n), 1 if reset else 0),
+               "wsg_timing_read")
+        return ms.value, n.value
 
     def encode_gather(self, n_total, chunk, payloads, descs, wires, wire_offs, root=0, out=None, out_off=None):
         """Per local rank (lists of CUDA tensors): payload arena, descriptor

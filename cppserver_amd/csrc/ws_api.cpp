@@ -48,8 +48,8 @@ bool receive_message(std::vector<uint8_t>& out, Required required, Prepare prepa
 
 void WSClient::ResetBuffers()
 {
-    if (_rx_batch)
-        _rx_batch->Clear(*this);   // message state resets in delivery order
+    if (WSReceiveBatch* b = _rx_batch.load(std::memory_order_acquire))
+        b->Clear(*this);   // message state resets in delivery order
     else if (BatchScope::Active())
         BatchScope::Receive().Clear(*this);
     else
@@ -64,9 +64,11 @@ WSClient::~WSClient()
 
 void WSClient::SetReceiveBatch(WSReceiveBatch* batch)
 {
-    if (_rx_batch && _rx_batch != batch)
-        _rx_batch->Forget(*this);
-    _rx_batch = batch;
+    // swapped atomically (the IO thread reads it per read); the old batch
+    // drops this connection's frames after the swap
+    WSReceiveBatch* old = _rx_batch.exchange(batch, std::memory_order_acq_rel);
+    if (old && old != batch)
+        old->Forget(*this);
 }
 
 bool WSClient::Connect()
@@ -140,8 +142,8 @@ void WSClient::onReceived(const void* buffer, size_t size)
 
 void WSClient::RouteFrames(const void* buffer, size_t size)
 {
-    if (_rx_batch) {
-        _rx_batch->Feed(*this, buffer, size);
+    if (WSReceiveBatch* b = _rx_batch.load(std::memory_order_acquire)) {
+        b->Feed(*this, buffer, size);
     } else if (BatchScope::Active()) {
         BatchScope::Receive().Feed(*this, buffer, size);
         BatchScope::CheckLimits();
@@ -244,8 +246,8 @@ std::vector<uint8_t> WSClient::ReceiveBinary(const CppCommon::Timespan& timeout)
 
 void WSSession::ResetBuffers()
 {
-    if (_rx_batch)
-        _rx_batch->Clear(*this);   // message state resets in delivery order
+    if (WSReceiveBatch* b = _rx_batch.load(std::memory_order_acquire))
+        b->Clear(*this);   // message state resets in delivery order
     else if (BatchScope::Active())
         BatchScope::Receive().Clear(*this);
     else
@@ -260,9 +262,11 @@ WSSession::~WSSession()
 
 void WSSession::SetReceiveBatch(WSReceiveBatch* batch)
 {
-    if (_rx_batch && _rx_batch != batch)
-        _rx_batch->Forget(*this);
-    _rx_batch = batch;
+    // swapped atomically (the IO thread reads it per read); the old batch
+    // drops this connection's frames after the swap
+    WSReceiveBatch* old = _rx_batch.exchange(batch, std::memory_order_acq_rel);
+    if (old && old != batch)
+        old->Forget(*this);
 }
 
 bool WSSession::Connect()
@@ -319,8 +323,8 @@ void WSSession::onReceived(const void* buffer, size_t size)
 
 void WSSession::RouteFrames(const void* buffer, size_t size)
 {
-    if (_rx_batch) {
-        _rx_batch->Feed(*this, buffer, size);
+    if (WSReceiveBatch* b = _rx_batch.load(std::memory_order_acquire)) {
+        b->Feed(*this, buffer, size);
     } else if (BatchScope::Active()) {
         BatchScope::Receive().Feed(*this, buffer, size);
         BatchScope::CheckLimits();
@@ -421,6 +425,18 @@ std::vector<uint8_t> WSSession::ReceiveBinary(const CppCommon::Timespan& timeout
 
 // ---------------------------------------------------------------- WSServer
 
+std::shared_ptr<WSReceiveBatch> WSServer::rx_batch() const
+{
+    std::shared_lock<std::shared_mutex> locker(_sessions_lock);
+    return _rx_batch;
+}
+
+std::shared_ptr<WSSendBatch> WSServer::tx_batch() const
+{
+    std::shared_lock<std::shared_mutex> locker(_sessions_lock);
+    return _tx_batch;
+}
+
 void WSServer::AddSession(const std::shared_ptr<WSSession>& session)
 {
     std::unique_lock<std::shared_mutex> locker(_sessions_lock);
@@ -435,15 +451,22 @@ void WSServer::AddSession(const std::shared_ptr<WSSession>& session)
 void WSServer::RemoveSession(const std::shared_ptr<WSSession>& session)
 {
     bool detach = false;
+    std::shared_ptr<WSReceiveBatch> rx;
+    std::shared_ptr<WSSendBatch> tx;
     {
         std::unique_lock<std::shared_mutex> locker(_sessions_lock);
         detach = std::find(_sessions.begin(), _sessions.end(), session) != _sessions.end();
         _sessions.erase(std::remove(_sessions.begin(), _sessions.end(), session), _sessions.end());
         _snapshot = std::make_shared<const std::vector<std::shared_ptr<WSSession>>>(_sessions);
+        // the batches the session is attached to: an EnableBatch*(false)
+        // from now on does not see the session and must not free them under
+        // the detach below
+        rx = _rx_batch;
+        tx = _tx_batch;
     }
-    // its queued frames are dropped with it; outside the sessions lock: the
-    // batches' Forget waits for a flush on another thread, whose callbacks
-    // may take that lock (a Multicast from onWSReceived)
+    // its queued frames are dropped with it; outside the sessions lock: a
+    // batch's Forget may wait for a flush on another thread that is calling
+    // into this session, and whose callbacks may take that lock
     if (detach) {
         session->SetReceiveBatch(nullptr);
         session->SetSendBatch(nullptr);
@@ -456,22 +479,24 @@ void WSServer::EnableBatchReceive(bool on)
     if (on == (_rx_batch != nullptr))
         return;
     if (on) {
-        _rx_batch = std::make_unique<WSReceiveBatch>(nullptr);   // flushes decode on the flushing thread's codec
+        _rx_batch = std::make_shared<WSReceiveBatch>(nullptr);   // flushes decode on the flushing thread's codec
         if (!_batch_devices.empty())
             _rx_batch->SetDevices(_batch_devices);
         for (auto& s : _sessions)
             s->SetReceiveBatch(_rx_batch.get());
         return;
     }
-    // detach outside the sessions lock (see RemoveSession): each Forget
-    // waits for a flush in progress on another thread, so the batch is idle
-    // when it goes
-    std::unique_ptr<WSReceiveBatch> gone = std::move(_rx_batch);
+    // detach outside the sessions lock (see RemoveSession); a flush in
+    // progress on another thread holds its own reference (FlushReceived),
+    // so the batch is freed when its last user lets go, not here
+    std::shared_ptr<WSReceiveBatch> gone = std::move(_rx_batch);
     const auto sessions = _sessions;
     locker.unlock();
     for (auto& s : sessions)
         s->SetReceiveBatch(nullptr);
-    gone.reset();
+    // a read that picked the batch up before its session let go framed its
+    // frames into it: deliver them rather than lose them
+    gone->Flush();
 }
 
 void WSServer::SetBatchDevices(const std::vector<int>& devices)
@@ -486,33 +511,39 @@ void WSServer::SetBatchDevices(const std::vector<int>& devices)
 
 void WSServer::EnableBatchSend(bool on)
 {
-    if (!on && _tx_batch)
-        _tx_batch->Flush();   // nothing queued is lost
+    if (!on)
+        if (const auto b = tx_batch())
+            b->Flush();   // nothing queued is lost
     std::unique_lock<std::shared_mutex> locker(_sessions_lock);
     if (on == (_tx_batch != nullptr))
         return;
     if (on) {
-        _tx_batch = std::make_unique<WSSendBatch>(nullptr);
+        _tx_batch = std::make_shared<WSSendBatch>(nullptr);
         if (!_batch_devices.empty())
             _tx_batch->SetDevices(_batch_devices);
         for (auto& s : _sessions)
             s->SetSendBatch(_tx_batch.get());
         return;
     }
-    std::unique_ptr<WSSendBatch> gone = std::move(_tx_batch);
+    std::shared_ptr<WSSendBatch> gone = std::move(_tx_batch);
     const auto sessions = _sessions;
     locker.unlock();
     for (auto& s : sessions)
         s->SetSendBatch(nullptr);
-    gone.reset();
+    gone->Flush();   // frames queued between the flush above and the detach
 }
 
-size_t WSServer::FlushSend() { return _tx_batch ? _tx_batch->Flush() : 0; }
+size_t WSServer::FlushSend()
+{
+    const auto b = tx_batch();   // kept alive for the flush (see rx_batch)
+    return b ? b->Flush() : 0;
+}
 
 size_t WSServer::FlushReceived()
 {
     // not under _sessions_lock: callbacks may add or remove sessions
-    return _rx_batch ? _rx_batch->Flush() : 0;
+    const auto b = rx_batch();
+    return b ? b->Flush() : 0;
 }
 
 size_t WSServer::sessions() const
@@ -527,8 +558,8 @@ bool WSServer::Multicast(const void* buffer, size_t size)
         return true;
     if (buffer == nullptr)
         return false;
-    if (_tx_batch)
-        _tx_batch->Flush();   // queued frames precede the multicast on every session
+    if (const auto b = tx_batch())
+        b->Flush();   // queued frames precede the multicast on every session
     else if (BatchScope::Active())
         BatchScope::Send().Flush();
     std::shared_lock<std::shared_mutex> locker(_sessions_lock);
@@ -542,7 +573,8 @@ bool WSServer::Multicast(const void* buffer, size_t size)
 
 size_t WSServer::MulticastFrame(uint8_t opcode, const void* buffer, size_t size)
 {
-    WSSendBatch* batch = _tx_batch ? _tx_batch.get() : BatchScope::Active() ? &BatchScope::Send() : nullptr;
+    const std::shared_ptr<WSSendBatch> own = tx_batch();
+    WSSendBatch* batch = own ? own.get() : BatchScope::Active() ? &BatchScope::Send() : nullptr;
     if (batch && size) {
         // batched: the frame is encoded with the batch's other frames (one
         // GPU pass per tick, ws_multicast's `messages_rate` calls included)
@@ -569,7 +601,7 @@ size_t WSServer::MulticastFrame(uint8_t opcode, const void* buffer, size_t size)
                 }
             },
             key, opcode, false, buffer, size);
-        if (batch != _tx_batch.get())
+        if (batch != own.get())
             BatchScope::CheckLimits();
         return true;   // the reference returns Multicast()'s bool (ws_server.h:50-59)
     }

@@ -213,12 +213,22 @@ void WSReceiveBatch::Forget(WebSocket& ws)
                 r.ws = nullptr;
         return;
     }
-    // another thread is delivering: it drops ws's frames before its next
-    // record (after the callback it may be running now), then wakes us
+    // Another thread is delivering.  It drops ws's frames before its next
+    // record: the flush announces each record's connection in _busy and
+    // then looks for pending Forgets (both sequentially consistent, as here
+    // the flag is raised before _busy is read), so either it sees this
+    // Forget before it calls into ws again, or ws is what it announced.
+    // Only then is there anything to wait for: the callback it is running
+    // for ws itself.  A flush busy with other connections is not waited for
+    // (two threads' callbacks destroying each other's connections must not
+    // block on each other's whole flush).
     _pending.push_back(&ws);
-    _has_pending.store(true, std::memory_order_release);
-    const uint64_t at = _applied;
-    _applied_cv.wait(locker, [&] { return _applied != at; });
+    _has_pending.store(true, std::memory_order_seq_cst);
+    if (_busy.load(std::memory_order_seq_cst) != &ws)
+        return;
+    _waiters.fetch_add(1, std::memory_order_seq_cst);
+    _busy_cv.wait(locker, [&] { return !_flushing || _busy.load(std::memory_order_seq_cst) != &ws; });
+    _waiters.fetch_sub(1, std::memory_order_relaxed);
 }
 
 void WSReceiveBatch::ApplyPending(size_t from)
@@ -230,8 +240,6 @@ void WSReceiveBatch::ApplyPending(size_t from)
                 _spare.recs[r].ws = nullptr;
     _pending.clear();
     _has_pending.store(false, std::memory_order_relaxed);
-    ++_applied;
-    _applied_cv.notify_all();
 }
 
 size_t WSReceiveBatch::Flush()
@@ -252,8 +260,10 @@ size_t WSReceiveBatch::Flush()
         {
             std::scoped_lock locker(t->_lock);
             t->_flushing = false;
+            t->_busy.store(nullptr, std::memory_order_seq_cst);
             t->_spare.reset();
-            t->ApplyPending(0);   // nothing left to deliver: release any waiting Forget
+            t->ApplyPending(0);
+            t->_busy_cv.notify_all();   // nothing left to deliver: release any waiting Forget
         }
     } done{this};
 
@@ -292,7 +302,13 @@ size_t WSReceiveBatch::Flush()
     // b.recs is written only by this thread (its callbacks' Forget); other
     // threads' Forget()s are applied here, between two records
     for (size_t r = 0; r < b.recs.size(); ++r) {
-        if (_has_pending.load(std::memory_order_acquire)) {
+        // announce the connection, then look for Forgets (see Forget)
+        _busy.store(b.recs[r].ws, std::memory_order_seq_cst);
+        if (_waiters.load(std::memory_order_seq_cst)) {
+            std::scoped_lock locker(_lock);   // a Forget waiting for the previous connection may go
+            _busy_cv.notify_all();
+        }
+        if (_has_pending.load(std::memory_order_seq_cst)) {
             std::scoped_lock locker(_lock);
             ApplyPending(r);
         }
@@ -418,10 +434,17 @@ void WSSendBatch::ForgetIf(Transport* transport, void* tag)
                 r = Rec{nullptr, nullptr, nullptr};
         return;
     }
-    _pending.emplace_back(transport, tag);   // applied by the flush before its next frame
-    _has_pending.store(true, std::memory_order_release);
-    const uint64_t at = _applied;
-    _applied_cv.wait(locker, [&] { return _applied != at; });
+    // applied by the flush before its next frame; waited for only while the
+    // flush is handing a frame to this very transport / tag (as
+    // WSReceiveBatch::Forget)
+    _pending.emplace_back(transport, tag);
+    _has_pending.store(true, std::memory_order_seq_cst);
+    const void* mine = transport ? static_cast<const void*>(transport) : tag;
+    if (_busy.load(std::memory_order_seq_cst) != mine)
+        return;
+    _waiters.fetch_add(1, std::memory_order_seq_cst);
+    _busy_cv.wait(locker, [&] { return !_flushing || _busy.load(std::memory_order_seq_cst) != mine; });
+    _waiters.fetch_sub(1, std::memory_order_relaxed);
 }
 
 void WSSendBatch::ApplyPending(size_t from)
@@ -435,8 +458,6 @@ void WSSendBatch::ApplyPending(size_t from)
         }
     _pending.clear();
     _has_pending.store(false, std::memory_order_relaxed);
-    ++_applied;
-    _applied_cv.notify_all();
 }
 
 size_t WSSendBatch::Flush(Sink sink, void* user)
@@ -458,10 +479,12 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
         {
             std::scoped_lock locker(t->_lock);
             t->_flushing = false;
+            t->_busy.store(nullptr, std::memory_order_seq_cst);
             t->_inflight.payload.len = 0;
             t->_inflight.desc.clear();
             t->_inflight.recs.clear();
-            t->ApplyPending(0);   // nothing left to hand out: release any waiting Forget
+            t->ApplyPending(0);
+            t->_busy_cv.notify_all();   // nothing left to hand out: release any waiting Forget
         }
     } done{this};
     Queue_& b = _inflight;
@@ -533,7 +556,16 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
     for (uint32_t i = 0; i < n; ++i) {
         const uint8_t* f = _wire.p + _wire_off[i];
         const size_t len = size_t(_wire_off[i + 1] - _wire_off[i]);
-        if (_has_pending.load(std::memory_order_acquire)) {
+        {
+            const Rec& next = b.recs[i];
+            _busy.store(next.transport ? static_cast<const void*>(next.transport) : next.tag,
+                        std::memory_order_seq_cst);
+        }
+        if (_waiters.load(std::memory_order_seq_cst)) {
+            std::scoped_lock locker(_lock);
+            _busy_cv.notify_all();
+        }
+        if (_has_pending.load(std::memory_order_seq_cst)) {
             std::scoped_lock locker(_lock);
             ApplyPending(i);
         }
@@ -591,6 +623,23 @@ struct AutoState {
         reg.erase(std::remove_if(reg.begin(), reg.end(), [](const AutoEntry& e) { return e.rx.expired(); }),
                   reg.end());
         reg.push_back(AutoEntry{rx_, tx_});
+    }
+    // The thread is ending: its entry goes under the registry lock, so that a
+    // ForgetEverywhere on another thread either still finds the batches (and
+    // synchronizes with their last flush through their lock) or comes after
+    // this point (and after every delivery this thread made).  An expired
+    // weak_ptr alone orders nothing.
+    ~AutoState()
+    {
+        std::lock_guard<std::mutex> g(auto_registry_lock());
+        auto& reg = auto_registry();
+        const WSReceiveBatch* mine = rx_.get();
+        reg.erase(std::remove_if(reg.begin(), reg.end(),
+                                 [&](const AutoEntry& e) {
+                                     const auto p = e.rx.lock();
+                                     return !p || p.get() == mine;
+                                 }),
+                  reg.end());
     }
 };
 

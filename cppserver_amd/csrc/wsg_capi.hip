@@ -483,6 +483,10 @@ int ensure_enc(const wsg_ctx* c, wsg_enc_scratch& e, uint32_t n, uint64_t wire_c
         return rc;
     if (c && small_path(c, n, wire_cap))
         return WSG_OK;
+    // pieces are indexed by u32 in the launch (q_begin / q_end): a bound past
+    // that (a wire_cap of terabytes, far past any HBM) is refused, not wrapped
+    if (pieces_bound(n, wire_cap) > UINT32_MAX)
+        return WSG_EINVAL;
     return ensure_array(e.d_piece_frame, e.piece_frame_cap, pieces_bound(n, wire_cap));
 }
 
@@ -498,6 +502,8 @@ int encode_launch(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, const wsg
         return WSG_OK;
     }
     const uint64_t pieces_cap = pieces_bound(n, wire_cap);
+    if (pieces_cap > UINT32_MAX)   // as ensure_enc: u32 piece indices below
+        return WSG_EINVAL;
     WSG_HIP(wsg::launch_encode_scan(s, d_desc, n, d_wire_off, e.d_piece_start, e.d_scan, e.d_piece_frame, pieces_cap,
                                     wire_cap, err));
     // one launch per run of at most enc_launch_pieces pieces (0: one launch)

@@ -93,6 +93,8 @@ hipError_t launch_xor(hipStream_t s, int grid, const uint8_t* src, uint8_t* dst,
 // out_off[n_total] = total.
 hipError_t launch_rebase_offsets(hipStream_t s, const uint64_t* stage, const uint64_t* goff, const uint64_t* rank_base,
                                  uint64_t n_total, uint32_t chunk, uint32_t world, uint64_t* out_off, uint64_t total);
+// Test hook only: one wave waiting `us` microseconds (at most 0.2 s) on `s`.
+hipError_t launch_test_spin(hipStream_t s, uint32_t us);
 
 // HIP device a context is bound to (wsg_capi.hip)
 int ctx_device(const wsg_ctx* c);

@@ -2061,6 +2061,30 @@ hipError_t launch_rebase_offsets(hipStream_t s, const uint64_t* stage, const uin
     return hipGetLastError();
 }
 
+// Test hook of the multi-GPU gather ($WSG_TEST_NULL_SPIN_US, wsg_mgpu.cpp):
+// one wave that waits `ticks` of the constant-rate wall clock on the stream
+// it is launched on.  The iteration cap ends it whatever the clock does
+// (about 2 s at the most).
+__global__ __launch_bounds__(64) void k_test_spin(uint64_t ticks)
+{
+    const uint64_t t0 = wall_clock64();
+    for (uint32_t i = 0; i < (1u << 20); ++i) {
+        if (wall_clock64() - t0 >= ticks)
+            break;
+        __builtin_amdgcn_s_sleep(64);
+    }
+}
+
+hipError_t launch_test_spin(hipStream_t s, uint32_t us)
+{
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+        khz = 100000;   // 100 MHz, the gfx9 constant clock
+    k_test_spin<<<1, 64, 0, s>>>(uint64_t(std::min<uint32_t>(us, 200000u)) * uint64_t(khz) / 1000u);
+    return hipGetLastError();
+}
+
 hipError_t launch_xor(hipStream_t s, int grid, const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,
                       uint32_t phase)
 {

@@ -97,6 +97,29 @@ const Rccl* rccl()
             return WSG_EHIP;                                                                                 \
     } while (0)
 
+// Test hook ($WSG_TEST_NULL_SPIN_US; tests/test_gpu_c5.py::
+// test_mgpu_rank_form_copy_ordering): before each host->device round of the
+// gather and before its transfers, park the device's null stream for that
+// long.  Plain hipMemcpy / hipMemset calls go to the null stream, which the
+// contexts' non-blocking streams do not wait for, so a copy that is not
+// ordered on the stream its consumer runs on lands after that consumer every
+// time instead of rarely.  Unset (the product): nothing is launched.
+uint32_t test_null_spin_us()
+{
+    static const uint32_t us = [] {
+        const char* e = std::getenv("WSG_TEST_NULL_SPIN_US");
+        return e ? uint32_t(std::strtoul(e, nullptr, 10)) : 0u;
+    }();
+    return us;
+}
+
+void test_park_null_stream(int device)
+{
+    if (const uint32_t us = test_null_spin_us())
+        if (hipSetDevice(device) == hipSuccess)
+            (void)wsg::launch_test_spin(nullptr, us);
+}
+
 inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
 // frames owned by `rank`: chunks r, r + world, ... of `chunk` frames each
@@ -455,6 +478,7 @@ int encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* 
         if (all_local)
             return status;
         for (Local& l : g->local) {
+            test_park_null_stream(l.device);
             WSG_HIP(hipSetDevice(l.device));
             const uint64_t mine = uint64_t(uint32_t(-status));
             // on the stream the all-gather runs on, landed before it (host
@@ -550,6 +574,7 @@ int encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* 
     } else {
         for (size_t i = 0; i < nl; ++i) {
             Local& l = g->local[i];
+            test_park_null_stream(l.device);
             WSG_HIP(hipSetDevice(l.device));
             WSG_HIP(hipMemcpyAsync(l.d_sizes, sizes[i].data(), maxq * sizeof(uint64_t), hipMemcpyHostToDevice,
                                    stream_of(l)));
@@ -576,6 +601,7 @@ int encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* 
     if (root_l && total > out_cap)
         fail(WSG_ENOMEM);
     if (root_l && !status) {
+        test_park_null_stream(root_l->device);
         // on the root's stream (k_rebase_offsets reads it there), landed
         // before the host vector goes
         if (hipSetDevice(root_l->device) != hipSuccess ||
@@ -594,6 +620,7 @@ int encode_gather(wsg_mgpu* g, uint64_t n_total, uint32_t chunk, const uint8_t* 
     // Per group: one data transfer per chunk (the output is in job order, a
     // rank's chunks are not adjacent there) + one offsets transfer per rank.
     for (Local& l : g->local) {
+        test_park_null_stream(l.device);
         WSG_HIP(hipSetDevice(l.device));
         WSG_HIP(hipEventRecord(l.e3, stream_of(l)));
     }

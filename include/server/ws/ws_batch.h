@@ -19,11 +19,14 @@
  * may come from any thread (a mutex guards the queue, as the reference's
  * per-session strands and locks let any IO thread call in); a Flush runs on
  * the calling thread with that thread's GPU codec context unless the batch
- * was given one, and fires the callbacks on that thread.  Forget(ws) from
- * another thread while a flush is delivering waits until the flush has
- * dropped ws's remaining frames (after the callback it may be running for
- * ws returns), so ws can be destroyed as soon as Forget returns; from
- * inside a callback of the flush it takes effect at once.
+ * was given one, and fires the callbacks on that thread.  Forget(ws) drops
+ * ws's frames at once and never waits for the rest of a flush: from another
+ * thread it waits only while that flush is inside a callback FOR ws itself
+ * (ws must outlive a call into it), so ws can be destroyed as soon as Forget
+ * returns; from inside a callback of the flush it takes effect at once.  Two
+ * threads whose callbacks each destroy a connection the other is delivering
+ * to are therefore never blocked on each other, only a thread destroying the
+ * very connection another thread is calling into is.
  */
 #ifndef CPPSERVER_AMD_WS_BATCH_H
 #define CPPSERVER_AMD_WS_BATCH_H
@@ -118,9 +121,10 @@ private:
     std::thread::id _flusher;
     std::vector<WebSocket*> _pending;    // other threads' Forget()s the flush has not applied yet
     std::atomic<bool> _has_pending{false};
-    uint64_t _applied = 0;               // ApplyPending rounds (a waiting Forget returns after the next)
-    std::condition_variable _applied_cv;
-    mutable std::mutex _lock;   // _cur, _flushing, _pending, _applied
+    std::atomic<const void*> _busy{nullptr};   // the connection the flush is at (announced before its Forget check)
+    std::atomic<int> _waiters{0};              // Forget()s waiting for _busy to move on
+    std::condition_variable _busy_cv;
+    mutable std::mutex _lock;   // _cur, _flushing, _pending
 };
 
 class Transport;
@@ -209,9 +213,10 @@ private:
     std::thread::id _flusher;
     std::vector<std::pair<Transport*, void*>> _pending;   // other threads' Forget()s not applied yet
     std::atomic<bool> _has_pending{false};
-    uint64_t _applied = 0;
-    std::condition_variable _applied_cv;
-    mutable std::mutex _lock;   // _q, _flushing, _pending, _applied
+    std::atomic<const void*> _busy{nullptr};   // transport / tag the flush is at (see WSReceiveBatch)
+    std::atomic<int> _waiters{0};
+    std::condition_variable _busy_cv;
+    mutable std::mutex _lock;   // _q, _flushing, _pending
 };
 
 /*

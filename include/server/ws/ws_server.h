@@ -52,7 +52,7 @@ public:
     //! bytes are framed into one WSReceiveBatch and unmasked in one GPU pass
     //! per FlushReceived(), which fires the sessions' onWS* in arrival order.
     void EnableBatchReceive(bool on);
-    bool IsBatchReceive() const { return _rx_batch != nullptr; }
+    bool IsBatchReceive() const { return rx_batch() != nullptr; }
     //! Decode and deliver everything the sessions received since the last
     //! flush; returns the number of frames delivered
     size_t FlushReceived();
@@ -61,7 +61,7 @@ public:
     //! are encoded in one GPU pass per FlushSend() and handed to their
     //! transports in queue order.  Multicast* flushes it first (order).
     void EnableBatchSend(bool on);
-    bool IsBatchSend() const { return _tx_batch != nullptr; }
+    bool IsBatchSend() const { return tx_batch() != nullptr; }
     size_t FlushSend();
 
     //! The GPUs the batched flushes spread over (one run per device's PCIe
@@ -71,9 +71,14 @@ public:
 
 private:
     size_t MulticastFrame(uint8_t opcode, const void* buffer, size_t size);
+    // the server's batches, read under the sessions lock: a flush or a
+    // detaching session holds its own reference, so a batch that
+    // EnableBatch*(false) drops lives until the last of them is done with it
+    std::shared_ptr<WSReceiveBatch> rx_batch() const;
+    std::shared_ptr<WSSendBatch> tx_batch() const;
 
-    std::unique_ptr<WSReceiveBatch> _rx_batch;
-    std::unique_ptr<WSSendBatch> _tx_batch;
+    std::shared_ptr<WSReceiveBatch> _rx_batch;
+    std::shared_ptr<WSSendBatch> _tx_batch;
     std::vector<int> _batch_devices;
 
     mutable std::shared_mutex _sessions_lock;

@@ -102,7 +102,7 @@ protected:
 
 private:
     std::string _http_buf;   // upgrade request bytes until its header block is complete
-    WSReceiveBatch* _rx_batch{nullptr};
+    std::atomic<WSReceiveBatch*> _rx_batch{nullptr};   // swapped by SetReceiveBatch, read by the IO thread
     WSSendBatch* _tx_batch{nullptr};
     void ResetBuffers();
     void RouteFrames(const void* buffer, size_t size);

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <random>
 #include <thread>
@@ -236,11 +237,107 @@ static void test_session_destroyed_while_queued_elsewhere()
     }
 }
 
+// Two threads flushing at once, each from inside a callback destroying a
+// connection still queued in the OTHER thread's flush (a Forget
+// that waited for the other flush's next record deadlocked here: each thread
+// waited for the other, both inside a callback).  `automatic`: the batches
+// are the threads' own BatchScope batches and the connections go through
+// BatchScope::ForgetEverywhere, as ~WSSession / ~WSClient do.  A watchdog
+// ends the process if the two flushes do not finish.
+struct Trigger : Conn {
+    std::function<void()> on_first;
+    std::atomic<int> calls{0};
+
+protected:
+    void onWSReceived(const void* buffer, size_t size) override
+    {
+        Conn::onWSReceived(buffer, size);
+        if (calls.fetch_add(1) == 0 && on_first)
+            on_first();
+    }
+};
+
+static void test_cross_thread_destroy_in_callbacks(bool automatic)
+{
+    for (int iter = 0; iter < 50; ++iter) {
+        // per iteration on the heap (the sanitizers track a freed block; a
+        // stack slot reused by the next iteration's mutex they do not)
+        struct State {
+            WSReceiveBatch x{nullptr}, y{nullptr};
+            Trigger tx, ty;
+            Conn* vx = new Conn;   // queued behind tx on thread A, destroyed by thread B's callback
+            Conn* vy = new Conn;   // queued behind ty on thread B, destroyed by thread A's callback
+            Sink dummy;
+            std::mutex m;
+            std::condition_variable cv;
+            int inside = 0;
+            std::atomic<int> done{0};
+        };
+        auto st = std::make_unique<State>();
+        State& S = *st;
+        auto both_inside = [&] {   // both flushes are inside a callback before either destroys
+            std::unique_lock<std::mutex> g(S.m);
+            ++S.inside;
+            S.cv.notify_all();
+            // no timed wait: this ThreadSanitizer does not intercept the
+            // clock-based condition wait libstdc++ uses for wait_for (a false
+            // "double lock"); the watchdog below bounds the test instead
+            S.cv.wait(g, [&] { return S.inside == 2; });
+        };
+        auto destroy = [&](WSReceiveBatch& other, Conn*& victim) {
+            if (automatic)
+                BatchScope::ForgetEverywhere(*victim, S.dummy);
+            else
+                other.Forget(*victim);
+            delete victim;
+            victim = nullptr;
+        };
+        S.tx.on_first = [&] { both_inside(); destroy(S.y, S.vy); };
+        S.ty.on_first = [&] { both_inside(); destroy(S.x, S.vx); };
+        const std::vector<uint8_t> f = unmasked_frame(24, 0x33);
+        auto run = [&](WSReceiveBatch& mine, Trigger& t, Conn* v) {
+            if (automatic) {
+                BatchScope scope;
+                BatchScope::Receive().Feed(t, f.data(), f.size());
+                BatchScope::Receive().Feed(*v, f.data(), f.size());
+                // the scope's end flushes this thread's automatic batch
+            } else {
+                mine.Feed(t, f.data(), f.size());
+                mine.Feed(*v, f.data(), f.size());
+                mine.Flush();
+            }
+            ++S.done;
+        };
+        std::thread watchdog([&] {
+            for (int i = 0; i < 200 && S.done.load() < 2; ++i)
+                std::this_thread::sleep_for(std::chrono::milliseconds(100));
+            if (S.done.load() < 2) {
+                std::fprintf(stderr, "cross-thread destroy (%s): flushes blocked on each other\n",
+                             automatic ? "automatic" : "explicit");
+                std::_Exit(3);
+            }
+        });
+        Conn* vx0 = S.vx;
+        Conn* vy0 = S.vy;
+        std::thread a([&] { run(S.x, S.tx, vx0); });
+        std::thread b([&] { run(S.y, S.ty, vy0); });
+        a.join();
+        b.join();
+        watchdog.join();
+        CHECK(S.tx.calls.load() == 1 && S.ty.calls.load() == 1);
+        CHECK(S.vx == nullptr && S.vy == nullptr);   // destroyed, and never delivered to after (Conn checks)
+    }
+}
+
 int main()
 {
     test_receive_forget_while_flushing();
     test_send_forget_while_flushing();
     test_session_destroyed_while_queued_elsewhere();
+    if (!std::getenv("ONLY_AUTO"))
+        test_cross_thread_destroy_in_callbacks(false);
+    if (!std::getenv("ONLY_EXPLICIT"))
+        test_cross_thread_destroy_in_callbacks(true);
     std::printf("%d checks, %d failures\n", g_checks.load(), g_failures.load());
     return g_failures.load() == 0 ? 0 : 1;
 }

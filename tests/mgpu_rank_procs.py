@@ -139,6 +139,10 @@ def run_case(world, n, chunk, root=0, bad=None, seed=1, timeout=150):
 def main():
     big = "--big" in sys.argv
     cases = []
+    if "--ordering" in sys.argv:   # test_mgpu_rank_form_copy_ordering ($WSG_TEST_NULL_SPIN_US set)
+        cases.append(run_case(2, 9000, 1024, seed=2 * 7919 + 9000 + 1024))
+        print(json.dumps(dict(cases=cases)), flush=True)
+        return
     for world in (2, 3):
         for n, chunk in ((1000, 1), (5000, 700), (9000, 1024)):
             cases.append(run_case(world, n, chunk, seed=world * 7919 + n + chunk))

@@ -345,6 +345,42 @@ def test_mgpu_rank_form_real_rccl_processes():
 
 
 @pytest.mark.gpu
+def test_mgpu_rank_form_copy_ordering():
+    """Every host->device and device->device copy of the rank-form gather is
+    ordered on the stream its consumer runs on (commit 0b854e9; the round-3
+    flake: rc 0 on every rank, stale root offsets).  $WSG_TEST_NULL_SPIN_US
+    makes the library park the device's null stream for 50 ms before each
+    host->device round and before the transfers, so a plain hipMemcpy /
+    hipMemset (null stream, not ordered with the contexts' non-blocking
+    streams) lands after its consumer every time.  World 2 and 3 over the
+    loopback double (ranks as threads), world 2 over the real RCCL (ranks as
+    processes): the root's wire and offsets vs the oracle."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "tests", "cpp", "_build", "libloopback_rccl.so")
+    assert os.path.exists(lib), "build tests/cpp first (make -C tests/cpp)"
+    env = dict(os.environ, WSG_TEST_NULL_SPIN_US="50000")
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "mgpu_rank_job.py")], capture_output=True,
+                       text=True, timeout=200, env=dict(env, WSG_RCCL_LIB=lib, WSG_RANK_JOB="ordering"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(d["cases"]) == 2
+    for c in d["cases"]:
+        assert not c["hung"] and c["rc"] == [0] * c["world"] and c["wire_ok"] and c["off_ok"], c
+    assert d["loopback_errors"] == 0
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "mgpu_rank_procs.py"), "--ordering"],
+                       capture_output=True, text=True, timeout=200, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    (c,) = d["cases"]
+    assert not c["hung"] and [x.get("rc") for x in c["ranks"]] == [0, 0], c
+    assert c["ranks"][0]["wire_ok"] and c["ranks"][0]["off_ok"], c
+
+
+@pytest.mark.gpu
 def test_mgpu_c5_tool_world1():
     """tools/mgpu_c5.py (the C-ABI leg bench.py runs at N > 1) at world 1 on
     a reduced job: encode + gather through wsg_mgpu_create, root check."""

@@ -132,3 +132,32 @@ def test_prepared_launch_checks():
         assert rc == 0 and np.array_equal(out.cpu().numpy(), ref)
     finally:
         c.close()
+
+
+def test_encode_refuses_piece_bound_past_u32():
+    """a wire_cap whose piece bound passes 2^32 (the launch's u32
+    piece indices) is refused with WSG_EINVAL instead of wrapping q_end
+    below q_begin and skipping pieces silently."""
+    import torch
+
+    import cppserver_amd as ca
+    from cppserver_amd import workloads as wl
+
+    codec = ca.Codec(0)
+    rng = np.random.default_rng(3)
+    desc, total = wl.ragged_desc(rng, np.full(4, 70000))
+    payload = torch.from_numpy(wl.random_bytes(rng, total)).cuda()
+    d = ca.desc_to_tensor(desc, "cuda")
+    wire = torch.empty(4 * 70016, dtype=torch.uint8, device="cuda")
+    woff = torch.empty(5, dtype=torch.int64, device="cuda")
+    lib = ca.lib()
+    import ctypes
+
+    rc = lib.wsg_encode_batch(codec._ctx, ctypes.c_void_p(payload.data_ptr()), ctypes.c_void_p(d.data_ptr()), 4,
+                              ctypes.c_void_p(wire.data_ptr()), 1 << 45, ctypes.c_void_p(woff.data_ptr()),
+                              codec._stream(None))
+    assert rc == ca.WSG_EINVAL
+    w, off = codec.encode_batch(payload, d, wire=wire, wire_off=woff)   # a real capacity still encodes
+    codec.sync()
+    assert int(off[-1].item()) == int(ca.frame_sizes(desc).sum())
+    codec.close()
