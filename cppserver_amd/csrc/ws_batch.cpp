@@ -111,9 +111,11 @@ void WSReceiveBatch::Emit(WebSocket& ws, const uint8_t* frame, uint64_t total, u
     // masked frames (MASK bit) with a nonzero key need the unmask pass
     if ((frame[1] & 0x80) && (dst[hdr - 4] | dst[hdr - 3] | dst[hdr - 2] | dst[hdr - 1]))
         b.keyed = true;
-    b.recs.push_back(Rec{&ws, int64_t(b.fs.size()), ws._ws_opcode, (frame[0] & 0x80) != 0});
+    b.recs.push_back(Rec{&ws, int64_t(b.fs.size()), ws._ws_opcode, (frame[0] & 0x80) != 0, hdr});
     b.fs.push_back(b.wire.len);
     b.wire.len += total;
+    _n_frames.store(b.fs.size(), std::memory_order_relaxed);
+    _n_bytes.store(b.wire.len, std::memory_order_relaxed);
 }
 
 void WSReceiveBatch::Feed(WebSocket& ws, const void* buffer, size_t size)
@@ -195,7 +197,7 @@ void WSReceiveBatch::Clear(WebSocket& ws)
 {
     std::scoped_lock locker(_lock);
     ws.ClearWSBuffers();
-    _cur.recs.push_back(Rec{&ws, -1, 0, false});
+    _cur.recs.push_back(Rec{&ws, -1, 0, false, 0});
 }
 
 void WSReceiveBatch::Forget(WebSocket& ws)
@@ -250,6 +252,8 @@ size_t WSReceiveBatch::Flush()
             return 0;
         std::swap(_cur, _spare);
         _cur.reset();
+        _n_frames.store(0, std::memory_order_relaxed);
+        _n_bytes.store(0, std::memory_order_relaxed);
         _flushing = true;
         _flusher = std::this_thread::get_id();
     }
@@ -272,8 +276,8 @@ size_t WSReceiveBatch::Flush()
     if (n) {
         if (n > UINT32_MAX)
             throw std::length_error("WSReceiveBatch: more than 2^32-1 frames in one flush");
-        b.info.resize(n);
         if (b.keyed) {
+            b.info.resize(n);
             Grow(b.out, b.wire.len);
             payload_base = b.out.p;
             if (_devs.size() > 1)
@@ -284,20 +288,16 @@ size_t WSReceiveBatch::Flush()
                 check(wsg_decode_batch_host(_devs.size() == 1 ? _devs[0] : _ctx ? _ctx : ThreadCodec(), b.wire.p,
                                             b.wire.len, b.fs.data(), uint32_t(n), b.out.p, b.info.data()),
                       "wsg_decode_batch_host");
-        } else {
-            // no frame has a key to apply (unmasked frames, or key 0: the
-            // server-to-client direction of every reference session,
-            // ws.cpp:206): unmasking is the identity, exactly as the
-            // per-call path skips it, so the payloads are handed out where
-            // they lie in the batch; only the headers are read
-            payload_base = b.wire.p;
-            for (size_t i = 0; i < n; ++i) {
-                const uint64_t end = i + 1 < n ? b.fs[i + 1] : b.wire.len;
-                check(wsg_header_unpack(b.wire.p + b.fs[i], end - b.fs[i], &b.info[i]), "wsg_header_unpack");
-                b.info[i].payload_off += b.fs[i];
-            }
         }
+        // else: no frame has a key to apply (unmasked frames, or key 0: the
+        // server-to-client direction of every reference session, ws.cpp:206):
+        // unmasking is the identity, exactly as the per-call path skips it, so
+        // the payloads are handed out where they lie in the batch, at the
+        // header sizes the framer recorded (b.info is not used)
     }
+    const bool keyed = b.keyed;
+    if (!keyed)
+        payload_base = b.wire.p;
     size_t delivered = 0;
     // b.recs is written only by this thread (its callbacks' Forget); other
     // threads' Forget()s are applied here, between two records
@@ -319,10 +319,17 @@ size_t WSReceiveBatch::Flush()
             rec.ws->ResetMessage();
             continue;
         }
-        const wsg_recv_info& in = b.info[size_t(rec.frame)];
-        if (in.error)
-            throw std::runtime_error("WSReceiveBatch: decode rejected a framed frame");
-        rec.ws->DeliverFrame(rec.opcode, rec.fin, payload_base + in.payload_off, size_t(in.len));
+        const size_t f = size_t(rec.frame);
+        if (keyed) {
+            const wsg_recv_info& in = b.info[f];
+            if (in.error)
+                throw std::runtime_error("WSReceiveBatch: decode rejected a framed frame");
+            rec.ws->DeliverFrame(rec.opcode, rec.fin, payload_base + in.payload_off, size_t(in.len));
+        } else {
+            const uint64_t at = b.fs[f] + rec.hdr;
+            const uint64_t end = f + 1 < n ? b.fs[f + 1] : b.wire.len;
+            rec.ws->DeliverFrame(rec.opcode, rec.fin, payload_base + at, size_t(end - at));
+        }
         ++delivered;
     }
     return delivered;
@@ -388,6 +395,7 @@ void WSSendBatch::Push(Rec rec, uint32_t key, uint8_t opcode, bool mask, const v
     pl.len += size;
     _q.desc.push_back(d);
     _q.recs.push_back(std::move(rec));
+    Counted();
 }
 
 void WSSendBatch::Queue(Transport& transport, uint32_t key, uint8_t opcode, bool mask, const void* buffer,
@@ -470,6 +478,7 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
         _q.payload.len = 0;
         _q.desc.clear();
         _q.recs.clear();
+        Counted();
         _flushing = true;
         _flusher = std::this_thread::get_id();
     }
@@ -491,14 +500,19 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
     if (b.desc.size() > UINT32_MAX)
         throw std::length_error("WSSendBatch: more than 2^32-1 frames in one flush");
     const uint32_t n = uint32_t(b.desc.size());
-    uint64_t total = 0;
-    for (const wsg_send_desc& d : b.desc)
-        total += wsg_frame_size(d.opcode, d.mask, d.len, d.status);
-    grow_pinned(_wire.p, _wire.cap, 0, std::max<uint64_t>(total, 1));
+    // frame offsets (the host path's sizes; a keyed pass recomputes them
+    // on the device) and whether any frame has a key to apply
     _wire_off.resize(size_t(n) + 1);
+    uint64_t total = 0;
     bool keyed = false;
-    for (const wsg_send_desc& d : b.desc)
+    for (uint32_t i = 0; i < n; ++i) {
+        const wsg_send_desc& d = b.desc[i];
+        _wire_off[i] = total;
+        total += wsg_frame_size(d.opcode, d.mask, d.len, d.status);
         keyed = keyed || d.key != 0;
+    }
+    _wire_off[n] = total;
+    grow_pinned(_wire.p, _wire.cap, 0, std::max<uint64_t>(total, 1));
     int rc = WSG_OK;
     if (keyed) {
         if (_devs.size() > 1)
@@ -510,12 +524,10 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
     } else {
         // every frame has key 0 (server sessions, ws.cpp:206): the XOR is the
         // identity, as on the per-call path; header + status + payload copy
-        uint64_t at = 0;
         for (uint32_t i = 0; i < n; ++i) {
             const wsg_send_desc& d = b.desc[i];
-            _wire_off[i] = at;
-            uint8_t* f = _wire.p + at;
-            const uint64_t size = wsg_frame_size(d.opcode, d.mask, d.len, d.status);
+            uint8_t* f = _wire.p + _wire_off[i];
+            const uint64_t size = _wire_off[i + 1] - _wire_off[i];
             const int hdr = wsg_header_pack(d.opcode, d.mask, d.len, d.status, 0, f);
             const uint64_t prefix = size - uint64_t(hdr) - d.len;
             if (prefix) {
@@ -524,9 +536,7 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
             }
             if (d.len)
                 std::memcpy(f + hdr + prefix, b.payload.p + d.src_off, d.len);
-            at += size;
         }
-        _wire_off[n] = at;
     }
     if (rc != WSG_OK) {
         // nothing was handed out: the frames go back in front of anything
@@ -548,6 +558,7 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
         b.payload.len = 0;
         b.desc.clear();
         b.recs.clear();
+        Counted();
         check(rc, "wsg_encode_batch_host");
     }
     size_t sent = 0;
@@ -569,7 +580,7 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
             std::scoped_lock locker(_lock);
             ApplyPending(i);
         }
-        const Rec rec = b.recs[i];
+        const Rec& rec = b.recs[i];   // written by this thread only (ApplyPending above)
         if (rec.transport) {
             rec.transport->SendAsync(f, len);
             ++sent;

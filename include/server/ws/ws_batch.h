@@ -72,16 +72,11 @@ public:
     //! batch); empty: the batch's own context.  Not during a flush.
     void SetDevices(const std::vector<int>& devices);
 
-    size_t frames() const
-    {
-        std::scoped_lock l(_lock);
-        return _cur.fs.size();
-    }
-    uint64_t bytes() const
-    {
-        std::scoped_lock l(_lock);
-        return _cur.wire.len;
-    }
+    // queued frames / wire bytes (exact for the queueing thread; a snapshot
+    // for others): read on every queued frame (BatchScope::CheckLimits), so
+    // counters kept beside the queue instead of taking its lock
+    size_t frames() const { return _n_frames.load(std::memory_order_relaxed); }
+    uint64_t bytes() const { return _n_bytes.load(std::memory_order_relaxed); }
 
 private:
     struct Pinned {
@@ -93,6 +88,7 @@ private:
         int64_t frame;    // index into fs, or -1: message reset marker
         uint8_t opcode;   // _ws_opcode in force when the frame completed
         bool fin;
+        uint32_t hdr;     // header bytes of the frame (its payload follows them)
     };
     struct Batch {
         Pinned wire, out;
@@ -124,6 +120,8 @@ private:
     std::atomic<const void*> _busy{nullptr};   // the connection the flush is at (announced before its Forget check)
     std::atomic<int> _waiters{0};              // Forget()s waiting for _busy to move on
     std::condition_variable _busy_cv;
+    std::atomic<size_t> _n_frames{0};          // _cur.fs.size(), written under _lock
+    std::atomic<uint64_t> _n_bytes{0};         // _cur.wire.len, written under _lock
     mutable std::mutex _lock;   // _cur, _flushing, _pending
 };
 
@@ -173,16 +171,9 @@ public:
     //! the batch's own context.  Not during a flush.
     void SetDevices(const std::vector<int>& devices);
 
-    size_t frames() const
-    {
-        std::scoped_lock l(_lock);
-        return _q.desc.size();
-    }
-    uint64_t payload_bytes() const
-    {
-        std::scoped_lock l(_lock);
-        return _q.payload.len;
-    }
+    // as WSReceiveBatch::frames()
+    size_t frames() const { return _n_frames.load(std::memory_order_relaxed); }
+    uint64_t payload_bytes() const { return _n_bytes.load(std::memory_order_relaxed); }
 
 private:
     struct Pinned {
@@ -216,6 +207,13 @@ private:
     std::atomic<const void*> _busy{nullptr};   // transport / tag the flush is at (see WSReceiveBatch)
     std::atomic<int> _waiters{0};
     std::condition_variable _busy_cv;
+    std::atomic<size_t> _n_frames{0};   // _q.desc.size(), written under _lock
+    std::atomic<uint64_t> _n_bytes{0};  // _q.payload.len, written under _lock
+    void Counted()
+    {
+        _n_frames.store(_q.desc.size(), std::memory_order_relaxed);
+        _n_bytes.store(_q.payload.len, std::memory_order_relaxed);
+    }
     mutable std::mutex _lock;   // _q, _flushing, _pending
 };
 

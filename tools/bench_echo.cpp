@@ -54,6 +54,21 @@
 using namespace CppServer::WS;
 using Clock = std::chrono::steady_clock;
 
+#ifdef ECHO_HOSTONLY
+// no device needed: the batches' page-locked buffers from the heap (the
+// executable's definitions take the place of libwsg.so's)
+extern "C" int wsg_host_alloc(size_t bytes, void** out)
+{
+    *out = std::malloc(bytes ? bytes : 1);
+    return *out ? WSG_OK : WSG_ENOMEM;
+}
+extern "C" int wsg_host_free(void* p)
+{
+    std::free(p);
+    return WSG_OK;
+}
+#endif
+
 namespace {
 
 struct Pipe : Transport {
@@ -109,6 +124,12 @@ struct EchoClient : Base {
     }
     void onWSConnected(const CppServer::HTTP::HTTPResponse&) override
     {
+#ifdef ECHO_HOSTONLY
+        // measurement build (tools/_build/echo_hostonly): the client key set
+        // to 0, so no frame has bytes to XOR and no GPU pass runs; what is
+        // left is the API's host work (framing, delivery, queueing)
+        this->set_send_key(0);
+#endif
         for (size_t i = _messages; i > 0; --i)
             SendMessage();
     }
