@@ -395,3 +395,32 @@ def test_mgpu_c5_tool_world1():
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["root_check"] is True
     assert d["host_decode"].get("check") is True, d["host_decode"]
+
+
+@pytest.mark.gpu
+def test_bench_n2_c5_rank_form():
+    """bench.py at N = 2 (torchrun, ranks sharing the one GPU over RCCL's
+    socket transport, as the driver's N > 1 runs but on one card): its c5_job
+    leg is the product's RCCL rank form (wsg_mgpu_create_rank +
+    wsg_mgpu_encode_gather) on a reduced job, with a per-rank roofline, root
+    ingress and the root's oracle check; the run exits 0 only if every leg's
+    check holds."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WSG_BENCH_SHARE_DEVICES="1", WSG_C5_FRAMES="16384", WSG_BENCH_TORCH_GATHER="0",
+               WSG_BENCH_CAPI_RCCL="0", WSG_BENCH_HOST_LEGS="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(root, "bench.py"),
+                        "--gpus", "2", "--steps", "5", "--warmup", "2", "--no-extras"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout[-1500:], r.stderr[-3000:])
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["spot_check"] is True and line["failed_checks"] == []
+    c5 = line["c5_job"]
+    assert c5["root_check"] is True, c5
+    assert c5["path"].startswith("C-ABI rank form")
+    assert c5["roofline_per_rank"]["kernel"] == "k_encode_mask" and c5["roofline_per_rank"]["frac"] > 0
+    assert c5["bytes_into_root"] == 16384 // 2 * (16384 + 8)

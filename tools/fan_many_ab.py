@@ -22,7 +22,14 @@ import cppserver_amd as ca  # noqa: E402
 KNOBS = ("WSG_FAN_WAVES_PER_CU", "WSG_FAN_WPB")
 
 
+VAR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cppserver_amd", "_build", "var")
+
+
 def make(spec):
+    """spec: "NAME=V,..." environment knobs, or "lib:<variant>" (a build of
+    tools/build_variant.sh under cppserver_amd/_build/var)."""
+    if spec.startswith("lib:"):
+        return ca.Codec(0, lib_path=os.path.join(VAR, spec[4:], "libwsg.so"))
     for k in KNOBS:
         os.environ.pop(k, None)
     for kv in filter(None, spec.split(",")):

@@ -33,6 +33,7 @@ step echo_prof_100c 120 tools/_build/bench_echo_prof per_read 100 4 1000 32 3
 step echo_ref_1c 120 tools/_build/bench_echo_ref 1 1 1000 32 3
 step c3_enc_diag 300 python -u tools/c3_enc_diag.py
 step fan_many_ab 200 python -u tools/fan_many_ab.py
+step bench_n2_test 400 python -u -m pytest tests/test_gpu_c5.py -x -v --timeout 380 --timeout-method thread -k "bench_n2"
 if [ "${SKIP_BENCH:-0}" != "1" ]; then
 step bench_n2 900 env WSG_BENCH_SHARE_DEVICES=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 5
 fi
