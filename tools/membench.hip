@@ -658,7 +658,8 @@ int main(int argc, char** argv)
         // 1 KiB row per wave per pass (the period kernel) vs 2 / 4 / 16
         // consecutive rows per block, nontemporal vs write-through, over
         // several wave counts; b2b = launches back to back
-        const uint64_t bytes41 = 41040000ull / 1024 * 1024;
+        // (argv[1] MiB > 0: that many bytes instead, e.g. 626 = ws_multicast's 16-message tick)
+        const uint64_t bytes41 = (mib ? n16 * 16 : 41040000ull) / 1024 * 1024;
         uint8_t* d;
         CK(hipMalloc(&d, 2 * bytes41 + 4096));
         const uint64_t rows = bytes41 / 1024;
