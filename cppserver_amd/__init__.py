@@ -109,6 +109,7 @@ def lib(path=None):
         "wsg_timing_enable": (ci, [vp, ci]),
         "wsg_timing_read": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ci]),
         "wsg_timing_minmax": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+        "wsg_lane_stats": (ci, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(ci)]),
     }
     for name, (res, args) in sig.items():
         if path is not None and not hasattr(L, name):
@@ -369,6 +370,14 @@ class Codec:
         lo, hi = ctypes.c_double(), ctypes.c_double()
         _check(self._L.wsg_timing_minmax(self._ctx, ctypes.byref(lo), ctypes.byref(hi)), "wsg_timing_minmax")
         return lo.value, hi.value
+
+    def lane_stats(self):
+        """(requests, launches, running) of the context's host lane
+        (wsg_lane_stats: small page-locked host batches)."""
+        r, l, on = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+        _check(self._L.wsg_lane_stats(self._ctx, ctypes.byref(r), ctypes.byref(l), ctypes.byref(on)),
+               "wsg_lane_stats")
+        return r.value, l.value, on.value
 
     def timing_read(self, reset=True):
         ms, n = ctypes.c_double(), ctypes.c_uint64()

@@ -6,8 +6,10 @@
 #include "wsg_trace.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -101,6 +103,20 @@ struct wsg_ctx {
     // run concurrently while kernels run between them ($WSG_PIPE=slots: one
     // stream per slot instead, the earlier design, kept for A/B runs)
     hipStream_t s_h2d = nullptr, s_kern = nullptr, s_d2h = nullptr;
+    // the host lane (wsg_internal.h): page-locked host batches of at most
+    // lane_max wire bytes go to a resident one-workgroup kernel through a
+    // doorbell instead of a launch + synchronize ($WSG_LANE_MAX, 0 = never)
+    struct Lane {
+        wsg::LaneBell* bell = nullptr;   // page-locked, coherent
+        hipStream_t stream = nullptr;
+        bool running = false;            // launched, not yet seen leaving
+        bool broken = false;             // did not answer: the launch paths from now on
+        uint64_t seq = 0;
+        uint64_t launches = 0;           // kernel launches of the lane (wsg_lane_stats)
+    } lane;
+    uint64_t lane_max = 64 << 10;
+    uint32_t lane_idle_us = 2000;   // the lane leaves after this long without a request
+    int wall_khz = 100000;          // constant clock of the lane's idle limit
     // timing of the dominant kernel
     struct EvPair {
         hipEvent_t a, b;
@@ -261,6 +277,129 @@ bool in_alloc(const void* p, uint64_t bytes)
 
 } // namespace
 
+// ---- the host lane --------------------------------------------------------
+
+namespace {
+
+// Every context with a lane, so that a process ending without wsg_destroy
+// still stops them (the lanes also leave on their own after lane_idle_us).
+std::mutex& lane_registry_lock()
+{
+    static std::mutex* m = new std::mutex;   // leaked: used at exit
+    return *m;
+}
+std::vector<wsg_ctx*>& lane_registry()
+{
+    static auto* v = new std::vector<wsg_ctx*>;
+    return *v;
+}
+
+// Ask the lane to leave and wait until it has (its kernel has ended).
+void lane_stop(wsg_ctx* c)
+{
+    if (!c->lane.running)
+        return;
+    (void)hipSetDevice(c->device);
+    __atomic_store_n(&c->lane.bell->stop, 1u, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(c->lane.stream);
+    c->lane.running = false;
+}
+
+void lanes_at_exit()
+{
+    std::lock_guard<std::mutex> g(lane_registry_lock());
+    for (wsg_ctx* c : lane_registry())
+        lane_stop(c);
+}
+
+// Launch the lane if it is not running (first use, or it left idle).
+int lane_start(wsg_ctx* c)
+{
+    if (!c->lane.bell) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, sizeof(wsg::LaneBell), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return WSG_ENOMEM;
+        std::memset(p, 0, sizeof(wsg::LaneBell));
+        c->lane.bell = static_cast<wsg::LaneBell*>(p);
+        if (hipStreamCreateWithFlags(&c->lane.stream, hipStreamNonBlocking) != hipSuccess)
+            return WSG_EHIP;
+        static std::once_flag once;
+        std::call_once(once, [] { std::atexit(lanes_at_exit); });
+        std::lock_guard<std::mutex> g(lane_registry_lock());
+        lane_registry().push_back(c);
+    }
+    if (c->lane.running)
+        return WSG_OK;
+    wsg::LaneBell* b = c->lane.bell;
+    b->stop = 0;
+    b->exited = 0;
+    const uint64_t idle = uint64_t(c->lane_idle_us) * uint64_t(c->wall_khz) / 1000u;
+    if (wsg::launch_lane(c->lane.stream, b, idle) != hipSuccess)
+        return WSG_EHIP;
+    c->lane.running = true;
+    ++c->lane.launches;
+    return WSG_OK;
+}
+
+// One request on the lane; returns when it is answered.  WSG_EHIP when the
+// lane does not answer within seconds (it is then not used again).
+int lane_call(wsg_ctx* c, uint32_t op, uint32_t n, const uint64_t (&a)[6])
+{
+    if (c->lane.broken)
+        return WSG_EHIP;
+    if (int rc = lane_start(c))
+        return rc;
+    wsg::LaneBell* b = c->lane.bell;
+    b->op = op;
+    b->n = n;
+    for (int k = 0; k < 6; ++k)
+        b->a[k] = a[k];
+    const uint64_t want = ++c->lane.seq;
+    __atomic_store_n(&b->seq, want, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t i = 1;; ++i) {
+        if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == want)
+            return WSG_OK;
+        if ((i & 255) == 0) {
+            if (__atomic_load_n(&b->exited, __ATOMIC_ACQUIRE)) {
+                // it left (idle limit) before it saw this request: wait until
+                // its kernel has ended, then launch it again; the new one
+                // starts from `done` and takes the request
+                (void)hipStreamSynchronize(c->lane.stream);
+                c->lane.running = false;
+                if (int rc = lane_start(c))
+                    return rc;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+                c->lane.broken = true;
+                __atomic_store_n(&b->stop, 1u, __ATOMIC_RELEASE);
+                return WSG_EHIP;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+void lane_release(wsg_ctx* c)
+{
+    if (!c->lane.bell)
+        return;
+    {
+        std::lock_guard<std::mutex> g(lane_registry_lock());
+        auto& reg = lane_registry();
+        reg.erase(std::remove(reg.begin(), reg.end(), c), reg.end());
+    }
+    if (!c->lane.broken)
+        lane_stop(c);
+    if (c->lane.stream)
+        (void)hipStreamDestroy(c->lane.stream);
+    if (!c->lane.running)   // (a lane that never answered may still read its doorbell)
+        (void)hipHostFree(c->lane.bell);
+    c->lane.bell = nullptr;
+}
+
+} // namespace
+
 extern "C" {
 
 int wsg_abi_version(void) { return WSG_ABI_VERSION; }
@@ -282,6 +421,7 @@ const char* wsg_strerror(int code)
         return "unknown error";
     }
 }
+
 
 int wsg_create(int device, wsg_ctx** out)
 {
@@ -342,6 +482,18 @@ int wsg_create(int device, wsg_ctx** out)
     }
     if (const char* e = std::getenv("WSG_SMALL_AVG"))   // A/B measurements (tools/tune_enc.py)
         c->small_avg = std::strtoull(e, nullptr, 10);
+    if (const char* e = std::getenv("WSG_LANE_MAX"))   // A/B measurements (tools/echo_size.py, bench_echo)
+        c->lane_max = std::strtoull(e, nullptr, 10);
+    if (const char* e = std::getenv("WSG_LANE_IDLE_US")) {
+        const long v = std::atol(e);
+        if (v > 0 && v <= 1000000)
+            c->lane_idle_us = uint32_t(v);
+    }
+    {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+            c->wall_khz = khz;
+    }
     *out = c;
     return WSG_OK;
 }
@@ -351,6 +503,7 @@ int wsg_destroy(wsg_ctx* c)
     if (!c)
         return WSG_EINVAL;
     (void)hipSetDevice(c->device);
+    lane_release(c);
     if (c->stream)
         (void)hipStreamSynchronize(c->stream);
     for (auto& ev : c->pending) {
@@ -897,6 +1050,14 @@ int host_batch_status(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const 
 // k_decode reads the wire and writes the output where they are, over PCIe,
 // on the context's stream — one launch and one synchronize instead of the
 // pipeline's H2D + kernel + D2H on three streams with event hand-offs.
+bool strictly_increasing(const uint64_t* v, uint32_t n)
+{
+    for (uint32_t i = 1; i < n; ++i)
+        if (v[i] <= v[i - 1])
+            return false;
+    return true;
+}
+
 int decode_host_direct(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start, uint32_t n,
                        uint8_t* out, wsg_recv_info* info)
 {
@@ -904,6 +1065,16 @@ int decode_host_direct(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const
     if (int rc = slot_reserve(sl, 0, n, false))
         return rc;
     std::memcpy(sl.h_fs, frame_start, size_t(n) * sizeof(uint64_t));
+    if (wire_len <= c->lane_max && n > 0 && strictly_increasing(frame_start, n)) {
+        // a few KiB (an echo's read): the resident lane, no launch
+        const uint64_t a[6] = {reinterpret_cast<uint64_t>(wire), wire_len, reinterpret_cast<uint64_t>(sl.h_fs),
+                               reinterpret_cast<uint64_t>(out), reinterpret_cast<uint64_t>(sl.h_info), 0};
+        if (lane_call(c, wsg::LANE_DECODE, n, a) == WSG_OK) {
+            std::memcpy(info, sl.h_info, size_t(n) * sizeof(wsg_recv_info));
+            return host_batch_status(c, wire, wire_len, frame_start, n, info);
+        }
+        // the lane did not answer: the launch path below (from now on always)
+    }
     hipStream_t s = c->stream;
     if (int rc = decode_launch(c, wire, wire_len, sl.h_fs, n, out, sl.h_info, s, c->d_err_host))
         return rc;
@@ -1099,6 +1270,17 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
             if (int rc = slot_reserve_enc(sl, 0, wire_off[n], n, false))
                 return rc;
             std::memcpy(sl.h_desc, desc, size_t(n) * sizeof(wsg_send_desc));
+            if (wire_off[n] <= c->lane_max) {
+                // a few KiB (the replies of an echo's read): the resident
+                // lane at the offsets computed above, no launch
+                if (int rc = slot_reserve(sl, 0, uint64_t(n) + 1, false))
+                    return rc;
+                std::memcpy(sl.h_fs, wire_off, (size_t(n) + 1) * sizeof(uint64_t));
+                const uint64_t a[6] = {reinterpret_cast<uint64_t>(payload), reinterpret_cast<uint64_t>(sl.h_desc),
+                                       reinterpret_cast<uint64_t>(sl.h_fs), reinterpret_cast<uint64_t>(wire), 0, 0};
+                if (lane_call(c, wsg::LANE_ENCODE, n, a) == WSG_OK)
+                    return WSG_OK;
+            }
             hipStream_t s = c->stream;
             if (int rc = encode_launch(c, s, payload, sl.h_desc, n, wire, wire_off[n], sl.d_woff, sl.enc,
                                        c->d_err_host))
@@ -1268,6 +1450,19 @@ int wsg_timing_read(wsg_ctx* c, double* total_ms, uint64_t* launches, int reset)
         c->launches = 0;
         c->min_ms = c->max_ms = 0.0;
     }
+    return WSG_OK;
+}
+
+int wsg_lane_stats(wsg_ctx* c, uint64_t* requests, uint64_t* launches, int* running)
+{
+    if (!c)
+        return WSG_EINVAL;
+    if (requests)
+        *requests = c->lane.seq;
+    if (launches)
+        *launches = c->lane.launches;
+    if (running)
+        *running = c->lane.broken ? -1 : c->lane.running ? 1 : 0;
     return WSG_OK;
 }
 

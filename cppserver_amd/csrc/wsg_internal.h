@@ -96,6 +96,33 @@ hipError_t launch_rebase_offsets(hipStream_t s, const uint64_t* stage, const uin
 // Test hook only: one wave waiting `us` microseconds (at most 0.2 s) on `s`.
 hipError_t launch_test_spin(hipStream_t s, uint32_t us);
 
+// ---- the host lane: a resident one-workgroup kernel for small host batches
+// A host batch of a few KiB (an echo's read: ~1000 frames of 38 B) costs a
+// launch and a synchronize per pass (10 us for an empty kernel on MI355X,
+// tools/smallpass.hip) on top of its PCIe round trips.  The lane is launched
+// once and waits on a doorbell in page-locked host memory: the host writes a
+// request and its sequence number, the lane does it on the host buffers in
+// place and answers with the number; the host spins on the answer.  Every
+// wave of it ends: on `stop`, or after idle_ticks of the constant clock with
+// no request (the host launches it again when it next rings).
+enum : uint32_t { LANE_DECODE = 1, LANE_ENCODE = 2 };
+constexpr uint32_t LANE_THREADS = 1024;   // one workgroup; frames per group (lane per frame)
+struct LaneBell {
+    uint64_t seq;       // host: request number (written last, release)
+    uint32_t op, n;     // host: LANE_* and frame count
+    uint64_t a[6];      // host: arguments (device-visible host addresses, sizes)
+    uint64_t pad0[8];
+    uint64_t done;      // lane: last request answered (release)
+    uint64_t pad1[7];
+    uint32_t stop;      // host: leave now
+    uint32_t exited;    // lane: has left (its last store)
+    uint64_t pad2[7];
+};
+// decode: a = {wire, wire_len, frame_start, out, info}; the table strictly
+//         increasing (the caller checks) — bit-identical to k_decode there
+// encode: a = {payload, desc, wire_off (n + 1, host-computed), wire}
+hipError_t launch_lane(hipStream_t s, LaneBell* bell, uint64_t idle_ticks);
+
 // HIP device a context is bound to (wsg_capi.hip)
 int ctx_device(const wsg_ctx* c);
 

@@ -1341,6 +1341,63 @@ __device__ __forceinline__ v4u small_bytes(const uint8_t* __restrict__ payload, 
     return out;
 }
 
+// A frame's head (header bytes + close status, <= 16 bytes: SURVEY Q2/Q3)
+// and record for the chunk builder; returns the frame's size.
+__device__ __forceinline__ uint64_t small_head(const Desc& d, v4u& h, SmallFrame& fr)
+{
+    const SendGeom g = send_geom(d.opcode, d.mask, d.len, d.status);
+    h = v4u{0, 0, 0, 0};
+#pragma unroll 1
+    for (uint32_t r = 0; r < g.hdr; ++r)
+        put_byte(h, r, header_byte(d.opcode, d.mask, g.body, d.key, r));
+    if (g.prefix) {   // close status, big-endian, masked like payload bytes 0-1
+        put_byte(h, g.hdr, uint32_t((d.status >> 8) & 0xFF) ^ key_byte(d.key, 0));
+        put_byte(h, g.hdr + 1, uint32_t(d.status & 0xFF) ^ key_byte(d.key, 1));
+    }
+    fr = SmallFrame{d.src_off, d.key, (g.hdr + g.prefix) | (g.hdr << 8)};
+    return g.hdr + g.body;
+}
+
+// The 16-B chunks of a group's wire range [s_off[0], s_off[cnt]) (frames
+// 0..cnt-1 of the group, LDS: offsets, heads, records), lanes t, t + nt, ...:
+// each chunk ORs together the frames it overlaps; only the range's first and
+// last chunk, shared with the neighbouring groups, get byte stores.
+__device__ __forceinline__ void small_chunks(const uint8_t* __restrict__ payload, const uint64_t* s_off,
+                                             const v4u* s_head, const SmallFrame* s_fr, uint32_t cnt,
+                                             uint8_t* __restrict__ wire, uint32_t t, uint32_t nt)
+{
+    const uint64_t r_lo = s_off[0], r_hi = s_off[cnt];
+    for (uint64_t p = (r_lo & ~uint64_t(CHUNK - 1)) + uint64_t(t) * CHUNK; p < r_hi; p += uint64_t(nt) * CHUNK) {
+        uint32_t a = 0, b = cnt - 1;   // last frame starting at or before p (frame 0 before the range)
+        while (a < b) {
+            const uint32_t m = (a + b + 1) >> 1;
+            if (s_off[m] <= p)
+                a = m;
+            else
+                b = m - 1;
+        }
+        v4u w = {0, 0, 0, 0};
+        for (uint32_t j = a; j < cnt; ++j) {
+            const uint64_t off = s_off[j];
+            if (off >= p + CHUNK)
+                break;
+            const uint64_t fsize = s_off[j + 1] - off;
+            if (p >= off)
+                w |= small_bytes(payload, s_head[j], s_fr[j], fsize, p - off);
+            else
+                w |= shl_bytes(small_bytes(payload, s_head[j], s_fr[j], fsize, 0), off - p);
+        }
+        if (p >= r_lo && p + CHUNK <= r_hi) {
+            st16nt(wire + p, w);
+        } else {
+            const uint32_t j0 = p < r_lo ? uint32_t(r_lo - p) : 0;
+            const uint32_t j1 = r_hi - p < CHUNK ? uint32_t(r_hi - p) : CHUNK;
+            for (uint32_t j = j0; j < j1; ++j)
+                wire[p + j] = uint8_t(lane_byte(w, j));
+        }
+    }
+}
+
 // Also finishes the offsets scan (k_encode_scan_blocks and
 // k_encode_finalize for the piece path): wire_off holds the block-local
 // offsets of k_encode_scan_local<false>, block_sums its nb block totals; a
@@ -1378,21 +1435,8 @@ __global__ __launch_bounds__(BLOCK) void k_encode_small(const uint8_t* __restric
         off_local = wire_off[f_lo + t];
     }
     uint64_t sz = 0;
-    if (t < cnt) {
-        const SendGeom g = send_geom(d.opcode, d.mask, d.len, d.status);
-        sz = g.hdr + g.body;
-        v4u h = {0, 0, 0, 0};
-#pragma unroll 1
-        for (uint32_t r = 0; r < g.hdr; ++r)
-            put_byte(h, r, header_byte(d.opcode, d.mask, g.body, d.key, r));
-        if (g.prefix) {   // close status, big-endian, masked like payload bytes 0-1
-            put_byte(h, g.hdr, uint32_t((d.status >> 8) & 0xFF) ^ key_byte(d.key, 0));
-            put_byte(h, g.hdr + 1, uint32_t(d.status & 0xFF) ^ key_byte(d.key, 1));
-        }
-        s_head[t] = h;
-        s_fr[t] = SmallFrame{d.src_off, d.key,
-                             (g.hdr + g.prefix) | (g.hdr << 8)};
-    }
+    if (t < cnt)
+        sz = small_head(d, s_head[t], s_fr[t]);
     uint64_t before = 0, all = 0;
 #pragma unroll
     for (int u = 0; u < PB; ++u) {
@@ -1425,37 +1469,169 @@ __global__ __launch_bounds__(BLOCK) void k_encode_small(const uint8_t* __restric
     __syncthreads();
     if (over)
         return;   // offsets are final and the error latched; no frame bytes
-    const uint64_t r_lo = s_off[0], r_hi = s_off[cnt];
-    for (uint64_t p = (r_lo & ~uint64_t(CHUNK - 1)) + uint64_t(threadIdx.x) * CHUNK; p < r_hi;
-         p += uint64_t(BLOCK) * CHUNK) {
-        uint32_t a = 0, b = cnt - 1;   // last frame starting at or before p (frame 0 before the range)
-        while (a < b) {
-            const uint32_t m = (a + b + 1) >> 1;
-            if (s_off[m] <= p)
-                a = m;
-            else
-                b = m - 1;
+    small_chunks(payload, s_off, s_head, s_fr, cnt, wire, threadIdx.x, BLOCK);
+}
+
+// ---- the host lane (wsg_internal.h) ----------------------------------------
+
+// Encode of a host batch on the lane: groups of LANE_THREADS frames, one
+// lane per frame builds its head (small_head), then the group's chunks
+// (small_chunks): the bytes k_encode_small writes, at the host's offsets.
+__device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload, const wsg_send_desc* __restrict__ desc,
+                                            uint32_t n, const uint64_t* __restrict__ wire_off,
+                                            uint8_t* __restrict__ wire, uint64_t* s_off, v4u* s_head,
+                                            SmallFrame* s_fr)
+{
+    const uint32_t t = threadIdx.x;
+    for (uint32_t f_lo = 0; f_lo < n; f_lo += LANE_THREADS) {
+        const uint32_t cnt = min(n - f_lo, LANE_THREADS);
+        if (t < cnt) {
+            const Desc d = load_desc(desc + f_lo + t);
+            s_off[t] = wire_off[f_lo + t];
+            (void)small_head(d, s_head[t], s_fr[t]);
+            if (t + 1 == cnt)
+                s_off[cnt] = wire_off[f_lo + cnt];
         }
-        v4u w = {0, 0, 0, 0};
-        for (uint32_t j = a; j < cnt; ++j) {
-            const uint64_t off = s_off[j];
-            if (off >= p + CHUNK)
-                break;
-            const uint64_t fsize = s_off[j + 1] - off;
-            if (p >= off)
-                w |= small_bytes(payload, s_head[j], s_fr[j], fsize, p - off);
-            else
-                w |= shl_bytes(small_bytes(payload, s_head[j], s_fr[j], fsize, 0), off - p);
+        __syncthreads();
+        small_chunks(payload, s_off, s_head, s_fr, cnt, wire, t, LANE_THREADS);
+        __syncthreads();   // the group's LDS is reused by the next
+    }
+}
+
+// Decode of a host batch on the lane (frame table strictly increasing):
+// groups of LANE_THREADS frames; a lane per frame parses it (frame_parse:
+// k_decode's rules) and writes its wsg_recv_info; then the group's wire range
+// — from its first frame's start (0 for the first group) to the next group's
+// (wire_len for the last) — goes out chunk by chunk: the wire bytes, the
+// valid frames' payload bytes XORed with their keys.  Out-of-range and
+// error frames' bytes are copied, as k_decode does.
+__device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, uint64_t wire_len,
+                                            const uint64_t* __restrict__ fs, uint32_t n, uint8_t* out,
+                                            wsg_recv_info* __restrict__ info, uint64_t* s_pl, uint64_t* s_pe,
+                                            uint32_t* s_key)
+{
+    const uint32_t t = threadIdx.x;
+    for (uint32_t f_lo = 0; f_lo < n; f_lo += LANE_THREADS) {
+        const uint32_t cnt = min(n - f_lo, LANE_THREADS);
+        if (t < cnt) {
+            const uint32_t i = f_lo + t;
+            const uint64_t st = fs[i];
+            const uint64_t limit = i + 1 < n ? fs[i + 1] : wire_len;
+            wsg_recv_info r;
+            const int e = frame_parse(wire, wire_len, st, limit, r);
+            store_info(info + i, r);
+            const uint64_t pl = e ? st : r.payload_off;
+            s_pl[t] = pl;
+            s_pe[t] = e ? st : pl + r.len;
+            s_key[t] = (e == 0 && r.masked) ? r.key : 0u;
         }
-        if (p >= r_lo && p + CHUNK <= r_hi) {
-            st16nt(wire + p, w);
-        } else {
-            const uint32_t j0 = p < r_lo ? uint32_t(r_lo - p) : 0;
-            const uint32_t j1 = r_hi - p < CHUNK ? uint32_t(r_hi - p) : CHUNK;
-            for (uint32_t j = j0; j < j1; ++j)
-                wire[p + j] = uint8_t(lane_byte(w, j));
+        __syncthreads();
+        const uint64_t lo = min(f_lo == 0 ? uint64_t(0) : fs[f_lo], wire_len);
+        const uint64_t hi = min(f_lo + cnt < n ? fs[f_lo + cnt] : wire_len, wire_len);
+        for (uint64_t p = (lo & ~uint64_t(CHUNK - 1)) + uint64_t(t) * CHUNK; p < hi; p += uint64_t(LANE_THREADS) * CHUNK) {
+            const v4u wv = ld16(wire + p);   // (a 16-B block never crosses a page)
+            // last frame whose payload starts at or before p (frame 0 if none)
+            uint32_t a = 0, b = cnt - 1;
+            while (a < b) {
+                const uint32_t m = (a + b + 1) >> 1;
+                if (s_pl[m] <= p)
+                    a = m;
+                else
+                    b = m - 1;
+            }
+            v4u m = {0, 0, 0, 0};
+            for (uint32_t j = a; j < cnt; ++j) {
+                const uint64_t pl = s_pl[j], pe = s_pe[j];
+                if (pl >= p + CHUNK)
+                    break;
+                const uint32_t key = s_key[j];
+                if (key == 0 || pe <= p)
+                    continue;
+                if (pl <= p && pe >= p + CHUNK) {   // the chunk lies in this payload
+                    const uint32_t kw = key_rot(key, uint32_t(p - pl));
+                    m ^= v4u{kw, kw, kw, kw};
+                } else {
+#pragma unroll 1
+                    for (uint32_t k = 0; k < CHUNK; ++k) {
+                        const uint64_t q = p + k;
+                        if (q >= pl && q < pe)
+                            put_byte(m, k, key_byte(key, q - pl));
+                    }
+                }
+            }
+            const v4u w = wv ^ m;
+            if (p >= lo && p + CHUNK <= hi) {
+                st16nt(out + p, w);
+            } else {
+                const uint32_t j0 = p < lo ? uint32_t(lo - p) : 0;
+                const uint32_t j1 = hi - p < CHUNK ? uint32_t(hi - p) : CHUNK;
+                for (uint32_t j = j0; j < j1; ++j)
+                    out[p + j] = uint8_t(lane_byte(w, j));
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ bell, uint64_t idle_ticks)
+{
+    __shared__ uint64_t s_a[6];
+    __shared__ uint32_t s_op, s_n;
+    __shared__ int s_go;
+    __shared__ uint64_t s_u0[LANE_THREADS + 1];   // encode: offsets; decode: payload starts
+    __shared__ uint64_t s_u1[LANE_THREADS];       // decode: payload ends
+    __shared__ uint32_t s_key[LANE_THREADS];
+    __shared__ v4u s_head[LANE_THREADS];
+    __shared__ SmallFrame s_fr[LANE_THREADS];
+    const uint32_t t = threadIdx.x;
+    uint64_t last = 0, seq = 0;
+    if (t == 0)
+        last = __hip_atomic_load(&bell->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (;;) {
+        if (t == 0) {
+            int go = 0;
+            const uint64_t t0 = wall_clock64();
+            // at most ~2^22 polls of >= 1 us each: ends even if the clock stalls
+            for (uint32_t it = 0; it < (1u << 22); ++it) {
+                seq = __hip_atomic_load(&bell->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (seq != last) {
+                    go = 1;
+                    break;
+                }
+                if (__hip_atomic_load(&bell->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                    wall_clock64() - t0 > idle_ticks)
+                    break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (go) {
+                s_op = __hip_atomic_load(&bell->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                s_n = __hip_atomic_load(&bell->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                for (int k = 0; k < 6; ++k)
+                    s_a[k] = __hip_atomic_load(&bell->a[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            s_go = go;
+        }
+        __syncthreads();
+        if (!s_go)
+            break;
+        const uint32_t op = s_op, n = s_n;
+        if (op == LANE_DECODE)
+            lane_decode(reinterpret_cast<const uint8_t*>(s_a[0]), s_a[1], reinterpret_cast<const uint64_t*>(s_a[2]), n,
+                        reinterpret_cast<uint8_t*>(s_a[3]), reinterpret_cast<wsg_recv_info*>(s_a[4]), s_u0, s_u1,
+                        s_key);
+        else if (op == LANE_ENCODE)
+            lane_encode(reinterpret_cast<const uint8_t*>(s_a[0]), reinterpret_cast<const wsg_send_desc*>(s_a[1]), n,
+                        reinterpret_cast<const uint64_t*>(s_a[2]), reinterpret_cast<uint8_t*>(s_a[3]), s_u0, s_head,
+                        s_fr);
+        __syncthreads();
+        if (t == 0) {
+            __threadfence_system();   // the request's stores are visible to the host before its answer
+            __hip_atomic_store(&bell->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            last = seq;
         }
     }
+    if (t == 0)
+        __hip_atomic_store(&bell->exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Grid = `main_blocks` streaming blocks, then the edge blocks.
@@ -2082,6 +2258,12 @@ hipError_t launch_test_spin(hipStream_t s, uint32_t us)
         hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
         khz = 100000;   // 100 MHz, the gfx9 constant clock
     k_test_spin<<<1, 64, 0, s>>>(uint64_t(std::min<uint32_t>(us, 200000u)) * uint64_t(khz) / 1000u);
+    return hipGetLastError();
+}
+
+hipError_t launch_lane(hipStream_t s, LaneBell* bell, uint64_t idle_ticks)
+{
+    k_lane<<<1, LANE_THREADS, 0, s>>>(bell, idle_ticks);
     return hipGetLastError();
 }
 

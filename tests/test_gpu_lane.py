@@ -1,0 +1,170 @@
+"""The host lane (wsg_lane_stats, wsg_internal.h): page-locked host batches
+of at most $WSG_LANE_MAX wire bytes go to a resident one-workgroup kernel
+through a doorbell in host memory instead of a launch per call.  Its bytes
+and per-frame fields must be those of the launch path and of the oracle,
+bit-exact:
+
+* many rounds through the SAME page-locked buffers with new bytes each time
+  (the lane never returns between requests: a stale cache line would show),
+  decode out of place and in place, encode, small frames to 64 KiB batches;
+* frame tables with errors (truncated last frame, a length running into the
+  next frame, a start past the wire) and tables the lane must not take
+  (not strictly increasing: the launch path);
+* the lane leaving after its idle limit and being launched again;
+* the lane against the launch path ($WSG_LANE_MAX=0) on the same batches."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import cppserver_amd as ca  # noqa: E402
+from cppserver_amd import workloads as wl  # noqa: E402
+from tests.test_gpu_parity import INFO_FIELDS  # noqa: E402
+
+OPCODES = [0x81, 0x82, 0x01, 0x88, 0x89, 0x8A, 0xC2]
+
+
+def _codec(**env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return ca.Codec(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def lane():
+    c = _codec(WSG_LANE_MAX=65536)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def launch():
+    c = _codec(WSG_LANE_MAX=0)
+    yield c
+    c.close()
+
+
+def _small_batch(rng, max_wire=60000):
+    n = int(rng.choice([1, 3, 40, 300, 1000, 1700]))
+    cls = rng.random(n)
+    lens = np.where(cls < 0.7, rng.integers(0, 126, n), np.where(cls < 0.97, rng.integers(126, 600, n),
+                                                                 rng.integers(600, 9000, n)))
+    while True:
+        desc, total = wl.ragged_desc(rng, lens)
+        desc["opcode"] = rng.choice(OPCODES, n)
+        desc["mask"] = rng.random(n) < 0.9
+        desc["status"] = np.where(rng.random(n) < 0.2, rng.integers(0, 70000, n), 0)
+        desc["src_off"] += rng.integers(0, 16, n).astype(np.uint64)
+        if int(ca.frame_sizes(desc).sum()) <= max_wire or n == 1:
+            break
+        lens = lens // 2
+    payload = wl.random_bytes(rng, total + 16)
+    return payload, desc
+
+
+def _check_decode(c, pin_in, wire, fs, pin_out=None):
+    rc_o, out_o, info_o = oracle.decode_batch(wire, fs)
+    pin_in[: len(wire)] = wire
+    rc, out, info = c.decode_batch_host(pin_in[: len(wire)], fs, out=pin_out if pin_out is not None else pin_in)
+    assert rc == rc_o
+    assert np.array_equal(out[: len(wire)], out_o)
+    for f in INFO_FIELDS:
+        assert np.array_equal(info[f], info_o[f]), f
+
+
+def test_lane_rounds_same_buffers(lane):
+    rng = np.random.default_rng(11)
+    pin_p, pin_w = ca.pinned_empty(1 << 17), ca.pinned_empty(1 << 17)
+    pin_in, pin_out = ca.pinned_empty(1 << 17), ca.pinned_empty(1 << 17)
+    r0, _, _ = lane.lane_stats()
+    for it in range(300):
+        payload, desc = _small_batch(rng)
+        wire_o, off_o = oracle.encode_batch(payload, desc)
+        pin_p[: len(payload)] = payload
+        rc, wire, off = lane.encode_batch_host(pin_p[: len(payload)], desc, wire=pin_w)
+        assert rc == 0 and np.array_equal(off, off_o) and np.array_equal(wire, wire_o), it
+        fs = off_o[:-1].copy()
+        _check_decode(lane, pin_in, wire_o, fs, pin_out)   # out of place
+        _check_decode(lane, pin_in, wire_o, fs)            # in place
+    r1, launches, running = lane.lane_stats()
+    assert r1 - r0 >= 3 * 300 - 5   # (a batch over the lane's size takes the launch path)
+    assert running in (0, 1)
+
+
+def test_lane_errors_and_tables(lane, launch):
+    rng = np.random.default_rng(5)
+    payload, desc = _small_batch(rng, max_wire=20000)
+    wire_o, off_o = oracle.encode_batch(payload, desc)
+    fs = off_o[:-1].copy()
+    pin = ca.pinned_empty(1 << 16)
+    pout = ca.pinned_empty(1 << 16)
+    cases = {
+        "truncated last": (wire_o[:-3], fs),
+        "start past the wire": (wire_o, np.concatenate([fs, [len(wire_o) + 40]]).astype(np.uint64)),
+        "frame runs into the next": (wire_o, np.sort(np.concatenate([fs, fs[-1:] + 1])).astype(np.uint64)),
+        "first frame not at 0": (np.concatenate([np.zeros(7, np.uint8), wire_o]), fs + np.uint64(7)),
+        "garbage starts": (wire_o, np.sort(rng.choice(len(wire_o), min(len(fs), 50), replace=False)).astype(np.uint64)),
+        "not increasing (launch path)": (wire_o, fs[::-1].copy()),
+        "repeated start (launch path)": (wire_o, np.concatenate([fs[:1], fs]).astype(np.uint64)),
+        "empty wire": (np.zeros(0, np.uint8), np.zeros(3, np.uint64)),
+    }
+    for name, (w, f) in cases.items():
+        rc_o, out_o, info_o = oracle.decode_batch(w, f)
+        for c in (lane, launch):
+            pin[: len(w)] = w
+            rc, out, info = c.decode_batch_host(pin[: len(w)], f, out=pout)
+            assert rc == rc_o, name
+            assert np.array_equal(out[: len(w)], out_o), name
+            for fld in INFO_FIELDS:
+                assert np.array_equal(info[fld], info_o[fld]), (name, fld)
+
+
+def test_lane_idle_relaunch():
+    c = _codec(WSG_LANE_MAX=65536, WSG_LANE_IDLE_US=500)
+    try:
+        rng = np.random.default_rng(9)
+        pin_in, pin_out = ca.pinned_empty(1 << 16), ca.pinned_empty(1 << 16)
+        for it in range(6):
+            payload, desc = _small_batch(rng, max_wire=30000)
+            wire_o, off_o = oracle.encode_batch(payload, desc)
+            _check_decode(c, pin_in, wire_o, off_o[:-1].copy(), pin_out)
+            time.sleep(0.01)   # 20 x the idle limit: the lane has left
+        req, launches, running = c.lane_stats()
+        assert req == 6 and launches >= 2, (req, launches)
+    finally:
+        c.close()
+
+
+def test_lane_matches_launch_path_echo_shape(lane, launch):
+    """The C1 echo's batches (1000 masked 38-byte frames; the replies of 1000
+    32-byte payloads) through both paths, bytes and fields equal."""
+    rng = np.random.default_rng(3)
+    desc, total = wl.ragged_desc(rng, np.full(1000, 32))
+    payload = wl.random_bytes(rng, total)
+    pin_p = ca.pinned_empty(total)
+    pin_p[:] = payload
+    outs = []
+    for c in (lane, launch):
+        pw = ca.pinned_empty(int(ca.frame_sizes(desc).sum()))
+        rc, w, off = c.encode_batch_host(pin_p, desc, wire=pw)
+        assert rc == 0
+        outs.append(np.array(w))
+    assert np.array_equal(outs[0], outs[1])
+    wire_o, off_o = oracle.encode_batch(payload, desc)
+    assert np.array_equal(outs[0], wire_o)
+    pin_in, pin_out = ca.pinned_empty(len(wire_o)), ca.pinned_empty(len(wire_o))
+    for c in (lane, launch):
+        _check_decode(c, pin_in, wire_o, off_o[:-1].copy(), pin_out)
