@@ -44,6 +44,12 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_ENC_NT_HI
 #define WSG_ENC_NT_HI 1    // ... including the funnel's second block (the next lane's line)
 #endif
+#ifndef WSG_LANE_DIAG
+#define WSG_LANE_DIAG 0   // timing-only host lane diagnostics: 1 answer without the work, 2 per-frame phase only
+#endif
+#ifndef WSG_ENC_EDGE
+#define WSG_ENC_EDGE 1   // k_encode_mask's non-data chunks: 1 byte loop (edge_chunk), 2 vector build + dword stores (edge_chunk2; A/B)
+#endif
 #ifndef WSG_DIAG_ENC
 #define WSG_DIAG_ENC 0   // timing-only encode diagnostics: 1 skip edge chunks, 2 no funnel
 #endif
@@ -885,6 +891,40 @@ static_assert(offsetof(wsg_send_desc, key) == 16 && offsetof(wsg_send_desc, opco
 
 __device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
+// 16 payload bytes as seen from a chunk: byte j = payload[c + j] where that
+// offset is inside [0, len) (else 0).  Reads only aligned 16-B blocks that
+// hold a wanted byte, at most two.
+__device__ __forceinline__ v4u fan_window(const uint8_t* __restrict__ payload, uint64_t len, int64_t c)
+{
+    // offsets relative to `payload`, loads through pointer arithmetic on it
+    // (global_* loads; a pointer rebuilt from an integer loads flat_*)
+    const uint32_t s = uint32_t((reinterpret_cast<uintptr_t>(payload) + uint64_t(c)) & 15u);
+    const int64_t r0 = c - int64_t(s);   // aligned block holding byte c, relative to payload
+    const int64_t n = int64_t(len);
+    v4u lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
+    if (r0 < n && r0 + 16 > 0)
+        lo = ld16(payload + r0);
+    if (s != 0 && r0 + 16 < n && r0 + 32 > 0)
+        hi = ld16(payload + r0 + 16);
+    return s ? funnel(lo, hi, s) : lo;
+}
+
+// 128-bit byte shifts and byte masks (runtime counts) built on funnel().
+__device__ __forceinline__ v4u shr_bytes(v4u x, uint64_t o)   // byte j = x[j + o]
+{
+    return o >= CHUNK ? v4u{0, 0, 0, 0} : funnel(x, v4u{0, 0, 0, 0}, uint32_t(o));
+}
+__device__ __forceinline__ v4u shl_bytes(v4u x, uint64_t s)   // byte j = x[j - s]
+{
+    return s == 0 ? x : s >= CHUNK ? v4u{0, 0, 0, 0} : funnel(v4u{0, 0, 0, 0}, x, uint32_t(CHUNK - s));
+}
+__device__ __forceinline__ v4u low_bytes(uint64_t n)   // bytes [0, n) = 0xFF
+{
+    const uint64_t lo = n >= 8 ? ~uint64_t(0) : (uint64_t(1) << (8 * n)) - 1;
+    const uint64_t hi = n >= 16 ? ~uint64_t(0) : n <= 8 ? 0 : (uint64_t(1) << (8 * (n - 8))) - 1;
+    return v4u{uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32)};
+}
+
 // A chunk of frame R that is not all data (it holds header / close-status
 // bytes, or it is shared with a neighbouring frame).  Its data bytes come
 // from one 32-byte source window read with at most two aligned 16-B loads
@@ -939,6 +979,59 @@ __device__ __forceinline__ void edge_chunk(const FrameRec& R, uint64_t p, uint8_
     }
 }
 
+// Header + close-status bytes of frame R (<= 16, as PrepareSendFrame writes
+// them, the status masked like payload bytes 0-1: SURVEY Q2/Q3), zero past
+// them; wave-uniform.
+__device__ __forceinline__ v4u frame_head(const FrameRec& R)
+{
+    v4u h = {0, 0, 0, 0};
+#pragma unroll 1
+    for (uint32_t r = 0; r < R.hdr; ++r)
+        put_byte(h, r, header_byte(R.opcode, R.mask, R.body, R.key, r));
+    if (R.prefix) {
+        put_byte(h, R.hdr, uint32_t((R.status >> 8) & 0xFF) ^ key_byte(R.key, 0));
+        put_byte(h, R.hdr + 1, uint32_t(R.status & 0xFF) ^ key_byte(R.key, 1));
+    }
+    return h;
+}
+
+// edge_chunk built with 16-byte vector operations instead of a byte loop:
+// the head shifted into place, the data window XORed with the rotated key
+// under its byte mask; stored whole when every byte is this frame's, else
+// by dwords (bytes only where a dword is shared with a neighbour).
+__device__ __forceinline__ void edge_chunk2(const FrameRec& R, v4u head, uint64_t p, uint8_t* __restrict__ wire)
+{
+    if (p + CHUNK <= R.off)
+        return;   // a chunk of the piece's line before the frame: a neighbour's
+    v4u w = p >= R.off ? shr_bytes(head, p - R.off) : shl_bytes(head, R.off - p);
+    const int64_t data_len = int64_t(R.end - R.data_w);
+    const int64_t rel = int64_t(p) - int64_t(R.data_w);   // source offset of chunk byte 0
+    if (rel < data_len && rel + int64_t(CHUNK) > 0) {
+        const v4u d = fan_window(R.src, uint64_t(data_len), rel);
+        const uint32_t kw = key_rot(R.key, uint32_t(p - R.pw));   // (mod 4 also when p < pw)
+        const uint64_t lo = p < R.data_w ? R.data_w - p : 0;
+        const uint64_t hi = R.end - p < CHUNK ? R.end - p : CHUNK;
+        w |= (d ^ v4u{kw, kw, kw, kw}) & (low_bytes(hi) & ~low_bytes(lo));
+    }
+    const uint32_t o_lo = p < R.off ? uint32_t(R.off - p) : 0u;
+    const uint32_t o_hi = R.end - p < CHUNK ? uint32_t(R.end - p) : uint32_t(CHUNK);
+    if ((o_lo == 0 && o_hi == CHUNK) || (WSG_DIAG_ENC & 4)) {
+        st16nt(wire + p, w);
+        return;
+    }
+    uint32_t* w32 = reinterpret_cast<uint32_t*>(wire + p);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t b0 = 4 * k, b1 = b0 + 4;
+        if (b0 >= o_lo && b1 <= o_hi) {
+            w32[k] = w[k];
+        } else {
+            for (uint32_t j = max(b0, o_lo); j < min(b1, o_hi); ++j)
+                wire[p + j] = uint8_t(w[k] >> (8 * (j - b0)));
+        }
+    }
+}
+
 // One wave's piece k of frame R, in two phases so that a wave can keep two
 // pieces' loads in flight before storing either (load(), then store()).
 template <bool NT>
@@ -988,13 +1081,20 @@ struct Piece {
             return;
         const uint32_t lane = threadIdx.x & 63;
         const OutTile ot(wire + lo, uint32_t(PIECE), WSG_ENC_SC1 != 0);
+        v4u head = {0, 0, 0, 0};
+        if (WSG_ENC_EDGE == 2 && lo < R.data_w)   // (wave-uniform) the piece holds header / status bytes
+            head = frame_head(R);
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
             const uint64_t p = lo + (uint64_t(u) * 64 + lane) * CHUNK;
             if ((dmask >> u) & 1u) {
                 ot.put(uint32_t(p - lo), (s ? funnel(a[u], b[u], s) : a[u]) ^ kw);
             } else if (p < hi && !(WSG_DIAG_ENC & 1)) {
-                edge_chunk(R, p, wire);   // header / status bytes, or a chunk shared with a neighbour
+                // header / status bytes, or a chunk shared with a neighbour
+                if (WSG_ENC_EDGE == 2)
+                    edge_chunk2(R, head, p, wire);
+                else
+                    edge_chunk(R, p, wire);
             }
         }
     }
@@ -1226,39 +1326,6 @@ __device__ __forceinline__ uint32_t fan_byte(const uint8_t* __restrict__ payload
     return uint32_t(payload[k - g.prefix]) ^ key_byte(key, k);
 }
 
-// 16 payload bytes as seen from a chunk: byte j = payload[c + j] where that
-// offset is inside [0, len) (else 0).  Reads only aligned 16-B blocks that
-// hold a wanted byte, at most two.
-__device__ __forceinline__ v4u fan_window(const uint8_t* __restrict__ payload, uint64_t len, int64_t c)
-{
-    // offsets relative to `payload`, loads through pointer arithmetic on it
-    // (global_* loads; a pointer rebuilt from an integer loads flat_*)
-    const uint32_t s = uint32_t((reinterpret_cast<uintptr_t>(payload) + uint64_t(c)) & 15u);
-    const int64_t r0 = c - int64_t(s);   // aligned block holding byte c, relative to payload
-    const int64_t n = int64_t(len);
-    v4u lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
-    if (r0 < n && r0 + 16 > 0)
-        lo = ld16(payload + r0);
-    if (s != 0 && r0 + 16 < n && r0 + 32 > 0)
-        hi = ld16(payload + r0 + 16);
-    return s ? funnel(lo, hi, s) : lo;
-}
-
-// 128-bit byte shifts and byte masks (runtime counts) built on funnel().
-__device__ __forceinline__ v4u shr_bytes(v4u x, uint64_t o)   // byte j = x[j + o]
-{
-    return o >= CHUNK ? v4u{0, 0, 0, 0} : funnel(x, v4u{0, 0, 0, 0}, uint32_t(o));
-}
-__device__ __forceinline__ v4u shl_bytes(v4u x, uint64_t s)   // byte j = x[j - s]
-{
-    return s == 0 ? x : s >= CHUNK ? v4u{0, 0, 0, 0} : funnel(v4u{0, 0, 0, 0}, x, uint32_t(CHUNK - s));
-}
-__device__ __forceinline__ v4u low_bytes(uint64_t n)   // bytes [0, n) = 0xFF
-{
-    const uint64_t lo = n >= 8 ? ~uint64_t(0) : (uint64_t(1) << (8 * n)) - 1;
-    const uint64_t hi = n >= 16 ? ~uint64_t(0) : n <= 8 ? 0 : (uint64_t(1) << (8 * (n - 8))) - 1;
-    return v4u{uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32)};
-}
 
 // Frames of one fan-out differ only in their key: the header + status bytes
 // (data0 <= 16 of them) are a constant vector plus the key bytes.
@@ -1493,7 +1560,8 @@ __device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload,
                 s_off[cnt] = wire_off[f_lo + cnt];
         }
         __syncthreads();
-        small_chunks(payload, s_off, s_head, s_fr, cnt, wire, t, LANE_THREADS);
+        if (WSG_LANE_DIAG != 2)   // (DIAG 2, timing only: the per-frame phase alone)
+            small_chunks(payload, s_off, s_head, s_fr, cnt, wire, t, LANE_THREADS);
         __syncthreads();   // the group's LDS is reused by the next
     }
 }
@@ -1526,6 +1594,8 @@ __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, ui
             s_key[t] = (e == 0 && r.masked) ? r.key : 0u;
         }
         __syncthreads();
+        if (WSG_LANE_DIAG == 2)   // timing only: the per-frame phase alone
+            continue;
         const uint64_t lo = min(f_lo == 0 ? uint64_t(0) : fs[f_lo], wire_len);
         const uint64_t hi = min(f_lo + cnt < n ? fs[f_lo + cnt] : wire_len, wire_len);
         for (uint64_t p = (lo & ~uint64_t(CHUNK - 1)) + uint64_t(t) * CHUNK; p < hi; p += uint64_t(LANE_THREADS) * CHUNK) {
@@ -1593,8 +1663,11 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
             const uint64_t t0 = wall_clock64();
             // at most ~2^22 polls of >= 1 us each: ends even if the clock stalls
             for (uint32_t it = 0; it < (1u << 22); ++it) {
-                seq = __hip_atomic_load(&bell->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                // polled relaxed, acquired once below (an acquire per poll
+                // would invalidate the caches on every iteration)
+                seq = __hip_atomic_load(&bell->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (seq != last) {
+                    __atomic_thread_fence(__ATOMIC_ACQUIRE);   // (system scope: the host's request bytes)
                     go = 1;
                     break;
                 }
@@ -1614,7 +1687,7 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
         __syncthreads();
         if (!s_go)
             break;
-        const uint32_t op = s_op, n = s_n;
+        const uint32_t op = WSG_LANE_DIAG == 1 ? 0u : s_op, n = s_n;   // DIAG 1: answer without the work (timing only)
         if (op == LANE_DECODE)
             lane_decode(reinterpret_cast<const uint8_t*>(s_a[0]), s_a[1], reinterpret_cast<const uint64_t*>(s_a[2]), n,
                         reinterpret_cast<uint8_t*>(s_a[3]), reinterpret_cast<wsg_recv_info*>(s_a[4]), s_u0, s_u1,

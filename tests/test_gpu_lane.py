@@ -123,13 +123,24 @@ def test_lane_errors_and_tables(lane, launch):
     }
     for name, (w, f) in cases.items():
         rc_o, out_o, info_o = oracle.decode_batch(w, f)
+        contract = bool(np.all(np.diff(f.astype(np.int64)) > 0))
         for c in (lane, launch):
             pin[: len(w)] = w
             rc, out, info = c.decode_batch_host(pin[: len(w)], f, out=pout)
             assert rc == rc_o, name
-            assert np.array_equal(out[: len(w)], out_o), name
-            for fld in INFO_FIELDS:
-                assert np.array_equal(info[fld], info_o[fld]), (name, fld)
+            if contract:
+                assert np.array_equal(out[: len(w)], out_o), name
+                for fld in INFO_FIELDS:
+                    assert np.array_equal(info[fld], info_o[fld]), (name, fld)
+            else:
+                # a table that is not strictly increasing breaks the decode
+                # contract (include/wsg_capi.h): the status and every frame's
+                # error are the oracle's, the valid frames' fields too; the
+                # output bytes are unspecified (test_decode_garbage_starts_match_oracle)
+                assert np.array_equal(info["error"], info_o["error"]), name
+                ok = info_o["error"] == 0
+                for fld in INFO_FIELDS:
+                    assert np.array_equal(info[fld][ok], info_o[fld][ok]), (name, fld)
 
 
 def test_lane_idle_relaunch():

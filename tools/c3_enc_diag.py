@@ -49,7 +49,8 @@ def batches():
 
 
 def main():
-    names = ["base"] + [v for v in ("diag1", "diag4", "diag2", "eu8", "eu2") if os.path.exists(os.path.join(VAR, v, "libwsg.so"))]
+    want = sys.argv[1:] or ["diag1", "diag4", "diag2", "eu8", "eu2"]
+    names = ["base"] + [v for v in want if os.path.exists(os.path.join(VAR, v, "libwsg.so"))]
     codecs = {n: ca.Codec(0) if n == "base" else ca.Codec(0, lib_path=os.path.join(VAR, n, "libwsg.so")) for n in names}
     out = {"variants": names, "batches": []}
     for name, payload, desc in batches():

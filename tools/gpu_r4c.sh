@@ -25,4 +25,8 @@ step echo_prof_100c 120 tools/_build/bench_echo_prof per_read 100 4 1000 32 3
 step echo_tick_100c 120 tools/_build/bench_echo tick 100 1 1000 32 3
 step echo_ref_1c 120 tools/_build/bench_echo_ref 1 1 1000 32 3
 step echo_ref_100c 120 tools/_build/bench_echo_ref 100 4 1000 32 3
+step edge2_parity 300 python -u tools/variant_parity.py edge2 300
+step edge2_diag 300 python -u tools/c3_enc_diag.py edge2 diag4
+step membench_wpattern 200 tools/_build/membench 626 wpattern
+step membench_write 200 tools/_build/membench 626 write
 echo "== done"
