@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -273,6 +274,47 @@ bool in_alloc(const void* p, uint64_t bytes)
         return false;
     const uintptr_t a = reinterpret_cast<uintptr_t>(p), b = reinterpret_cast<uintptr_t>(base);
     return a >= b && a - b <= size && bytes <= size - (a - b);
+}
+
+} // namespace
+
+namespace {
+
+// The blocks wsg_host_alloc made (page-locked, mapped at the same address on
+// the device): a host batch in one of them (the session batches' buffers
+// always are) is recognised without a runtime query, whose few us per
+// pointer were a visible share of a small batch's call (tools/lane_ab.py).
+// A block leaves the table before it is freed.
+std::mutex& host_blocks_lock()
+{
+    static std::mutex* m = new std::mutex;   // leaked: used from static destructors
+    return *m;
+}
+std::map<uintptr_t, uint64_t>& host_blocks()
+{
+    static auto* b = new std::map<uintptr_t, uint64_t>;
+    return *b;
+}
+void host_blocks_add(const void* p, uint64_t bytes)
+{
+    std::lock_guard<std::mutex> g(host_blocks_lock());
+    host_blocks()[reinterpret_cast<uintptr_t>(p)] = bytes;
+}
+void host_blocks_remove(const void* p)
+{
+    std::lock_guard<std::mutex> g(host_blocks_lock());
+    host_blocks().erase(reinterpret_cast<uintptr_t>(p));
+}
+bool in_host_block(const void* p)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> g(host_blocks_lock());
+    auto& m = host_blocks();
+    auto it = m.upper_bound(a);
+    if (it == m.begin())
+        return false;
+    --it;
+    return a - it->first < it->second;
 }
 
 } // namespace
@@ -866,6 +908,8 @@ namespace {
 
 bool host_pinned(const void* p)
 {
+    if (in_host_block(p))
+        return true;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
@@ -880,6 +924,8 @@ bool host_pinned(const void* p)
 // the staged pipeline (hipMemcpyAsync handles any host pointer).
 bool host_direct(const void* p)
 {
+    if (in_host_block(p))
+        return true;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
@@ -1007,12 +1053,16 @@ int wsg_host_alloc(size_t bytes, void** out)
     *out = nullptr;
     if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
         return WSG_ENOMEM;
+    host_blocks_add(*out, bytes ? bytes : 1);
     return WSG_OK;
 }
 
 int wsg_host_free(void* p)
 {
-    if (p && hipHostFree(p) != hipSuccess)
+    if (!p)
+        return WSG_OK;
+    host_blocks_remove(p);
+    if (hipHostFree(p) != hipSuccess)
         return WSG_EHIP;
     return WSG_OK;
 }
@@ -1065,7 +1115,7 @@ int decode_host_direct(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const
     if (int rc = slot_reserve(sl, 0, n, false))
         return rc;
     std::memcpy(sl.h_fs, frame_start, size_t(n) * sizeof(uint64_t));
-    if (wire_len <= c->lane_max && n > 0 && strictly_increasing(frame_start, n)) {
+    if (wire_len <= std::min<uint64_t>(c->lane_max, wsg::LANE_STAGE) && n > 0 && strictly_increasing(frame_start, n)) {
         // a few KiB (an echo's read): the resident lane, no launch
         const uint64_t a[6] = {reinterpret_cast<uint64_t>(wire), wire_len, reinterpret_cast<uint64_t>(sl.h_fs),
                                reinterpret_cast<uint64_t>(out), reinterpret_cast<uint64_t>(sl.h_info), 0};

@@ -107,6 +107,10 @@ hipError_t launch_test_spin(hipStream_t s, uint32_t us);
 // no request (the host launches it again when it next rings).
 enum : uint32_t { LANE_DECODE = 1, LANE_ENCODE = 2 };
 constexpr uint32_t LANE_THREADS = 1024;   // one workgroup; frames per group (lane per frame)
+constexpr uint64_t LANE_STAGE = 64 << 10;  // decode: wire bytes staged in LDS (the lane's batch limit)
+// LDS of the lane: decode's staged wire + info blocks + payload bounds and
+// keys; encode's offsets, heads, records and staged descriptors fit inside
+constexpr uint64_t LANE_LDS = LANE_STAGE + 32 * LANE_THREADS + 20 * LANE_THREADS;
 struct LaneBell {
     uint64_t seq;       // host: request number (written last, release)
     uint32_t op, n;     // host: LANE_* and frame count

@@ -48,7 +48,7 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #define WSG_LANE_DIAG 0   // timing-only host lane diagnostics: 1 answer without the work, 2 per-frame phase only
 #endif
 #ifndef WSG_ENC_EDGE
-#define WSG_ENC_EDGE 1   // k_encode_mask's non-data chunks: 1 byte loop (edge_chunk), 2 vector build + dword stores (edge_chunk2; A/B)
+#define WSG_ENC_EDGE 2   // k_encode_mask non-data chunks: 2 vector build + dword stores (edge_chunk2), 1 the byte loop (edge_chunk, A/B): C3 0.730 -> 0.701 ms (profiles/r4/edge2_diag.log)
 #endif
 #ifndef WSG_DIAG_ENC
 #define WSG_DIAG_ENC 0   // timing-only encode diagnostics: 1 skip edge chunks, 2 no funnel
@@ -312,8 +312,11 @@ __device__ __forceinline__ uint64_t uni(uint64_t x)
 // (ws.cpp:320-386), with the batch checks of wsg_decode_batch.  Returns 0 or
 // the frame's error; on error r describes an empty payload at s, so the
 // frame's bytes are copied.
-__device__ __forceinline__ int frame_parse(const uint8_t* __restrict__ wire, uint64_t wire_len, uint64_t s,
-                                           uint64_t limit, wsg_recv_info& r)
+// (Block16: the aligned 16-byte block at a wire offset; global memory here,
+// LDS for the host lane's staged wire.)
+template <class Block16>
+__device__ __forceinline__ int frame_parse_b(Block16 block, uint64_t wire_len, uint64_t s, uint64_t limit,
+                                             wsg_recv_info& r)
 {
     r = wsg_recv_info{};
     int e = WSG_ETRUNC;
@@ -322,8 +325,8 @@ __device__ __forceinline__ int frame_parse(const uint8_t* __restrict__ wire, uin
         // wire[s .. s+16) as two u64 from the aligned 32-byte window, with
         // 64-bit shifts only (scalar instructions when s is wave-uniform)
         const uint64_t a0 = s & ~uint64_t(15);
-        const v4u lo = ld16(wire + a0);
-        const v4u hi = (a0 + 16 < wire_len) ? ld16(wire + a0 + 16) : v4u{0, 0, 0, 0};
+        const v4u lo = block(a0);
+        const v4u hi = (a0 + 16 < wire_len) ? block(a0 + 16) : v4u{0, 0, 0, 0};
         uint64_t q0 = uint64_t(lo.x) | (uint64_t(lo.y) << 32), q1 = uint64_t(lo.z) | (uint64_t(lo.w) << 32);
         const uint64_t q2 = uint64_t(hi.x) | (uint64_t(hi.y) << 32), q3 = uint64_t(hi.z) | (uint64_t(hi.w) << 32);
         uint64_t q2s = q2;
@@ -351,6 +354,12 @@ __device__ __forceinline__ int frame_parse(const uint8_t* __restrict__ wire, uin
         r.payload_off = s + r.hdr_len;
     }
     return e;
+}
+
+__device__ __forceinline__ int frame_parse(const uint8_t* __restrict__ wire, uint64_t wire_len, uint64_t s,
+                                           uint64_t limit, wsg_recv_info& r)
+{
+    return frame_parse_b([wire](uint64_t a) { return ld16(wire + a); }, wire_len, s, limit, r);
 }
 
 // wsg_recv_info as four 8-byte words (a struct store of the byte fields went
@@ -1541,23 +1550,42 @@ __global__ __launch_bounds__(BLOCK) void k_encode_small(const uint8_t* __restric
 
 // ---- the host lane (wsg_internal.h) ----------------------------------------
 
-// Encode of a host batch on the lane: groups of LANE_THREADS frames, one
-// lane per frame builds its head (small_head), then the group's chunks
-// (small_chunks): the bytes k_encode_small writes, at the host's offsets.
+// The lane reads its host inputs in whole, coalesced 16-byte blocks into
+// LDS first: one workgroup has few memory requests in flight, and every
+// round trip over PCIe costs microseconds (a lane-per-frame read of 32-byte
+// descriptors or headers scattered over lines took several).
+__device__ __forceinline__ void lane_stage(v4u* dst, const uint8_t* __restrict__ src, uint64_t blocks)
+{
+    for (uint64_t c = threadIdx.x; c < blocks; c += LANE_THREADS)
+        dst[c] = ld16(src + c * CHUNK);
+}
+
+// Encode of a host batch on the lane: groups of LANE_THREADS frames; the
+// group's descriptors staged, one lane per frame builds its head
+// (small_head), then the group's chunks (small_chunks): the bytes
+// k_encode_small writes, at the host's offsets.
 __device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload, const wsg_send_desc* __restrict__ desc,
                                             uint32_t n, const uint64_t* __restrict__ wire_off,
-                                            uint8_t* __restrict__ wire, uint64_t* s_off, v4u* s_head,
-                                            SmallFrame* s_fr)
+                                            uint8_t* __restrict__ wire, uint8_t* lds)
 {
+    uint64_t* s_off = reinterpret_cast<uint64_t*>(lds);                             // LANE_THREADS + 1 (+1 pad)
+    v4u* s_head = reinterpret_cast<v4u*>(lds + 8 * (LANE_THREADS + 2));
+    SmallFrame* s_fr = reinterpret_cast<SmallFrame*>(s_head + LANE_THREADS);
+    v4u* s_desc = reinterpret_cast<v4u*>(s_fr + LANE_THREADS);                       // 2 blocks per descriptor
+    static_assert(sizeof(wsg_send_desc) == 32 && sizeof(SmallFrame) == 16, "lane LDS layout");
     const uint32_t t = threadIdx.x;
     for (uint32_t f_lo = 0; f_lo < n; f_lo += LANE_THREADS) {
         const uint32_t cnt = min(n - f_lo, LANE_THREADS);
+        lane_stage(s_desc, reinterpret_cast<const uint8_t*>(desc + f_lo), 2 * uint64_t(cnt));
         if (t < cnt) {
-            const Desc d = load_desc(desc + f_lo + t);
             s_off[t] = wire_off[f_lo + t];
-            (void)small_head(d, s_head[t], s_fr[t]);
             if (t + 1 == cnt)
                 s_off[cnt] = wire_off[f_lo + cnt];
+        }
+        __syncthreads();
+        if (t < cnt) {
+            const Desc d = load_desc(reinterpret_cast<const wsg_send_desc*>(s_desc) + t);
+            (void)small_head(d, s_head[t], s_fr[t]);
         }
         __syncthreads();
         if (WSG_LANE_DIAG != 2)   // (DIAG 2, timing only: the per-frame phase alone)
@@ -1566,19 +1594,28 @@ __device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload,
     }
 }
 
-// Decode of a host batch on the lane (frame table strictly increasing):
-// groups of LANE_THREADS frames; a lane per frame parses it (frame_parse:
-// k_decode's rules) and writes its wsg_recv_info; then the group's wire range
-// — from its first frame's start (0 for the first group) to the next group's
-// (wire_len for the last) — goes out chunk by chunk: the wire bytes, the
-// valid frames' payload bytes XORed with their keys.  Out-of-range and
-// error frames' bytes are copied, as k_decode does.
+// Decode of a host batch on the lane (frame table strictly increasing, the
+// wire at most LANE_STAGE bytes): the wire staged into LDS; groups of
+// LANE_THREADS frames, a lane per frame parses it (frame_parse_b: k_decode's
+// rules) into LDS, the group's wsg_recv_info go out in whole blocks; then the
+// group's wire range — from its first frame's start (0 for the first group)
+// to the next group's (wire_len for the last) — chunk by chunk: the wire
+// bytes, the valid frames' payload bytes XORed with their keys.  Out-of-range
+// and error frames' bytes are copied, as k_decode does.
 __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, uint64_t wire_len,
                                             const uint64_t* __restrict__ fs, uint32_t n, uint8_t* out,
-                                            wsg_recv_info* __restrict__ info, uint64_t* s_pl, uint64_t* s_pe,
-                                            uint32_t* s_key)
+                                            wsg_recv_info* __restrict__ info, uint8_t* lds)
 {
+    v4u* s_wire = reinterpret_cast<v4u*>(lds);
+    v4u* s_info = reinterpret_cast<v4u*>(lds + LANE_STAGE);                          // 2 blocks per record
+    uint64_t* s_pl = reinterpret_cast<uint64_t*>(s_info + 2 * LANE_THREADS);
+    uint64_t* s_pe = s_pl + LANE_THREADS;
+    uint32_t* s_key = reinterpret_cast<uint32_t*>(s_pe + LANE_THREADS);
+    static_assert(sizeof(wsg_recv_info) == 32, "lane LDS layout");
     const uint32_t t = threadIdx.x;
+    lane_stage(s_wire, wire, (wire_len + CHUNK - 1) / CHUNK);
+    __syncthreads();
+    const auto block = [s_wire](uint64_t a) { return s_wire[a / CHUNK]; };
     for (uint32_t f_lo = 0; f_lo < n; f_lo += LANE_THREADS) {
         const uint32_t cnt = min(n - f_lo, LANE_THREADS);
         if (t < cnt) {
@@ -1586,20 +1623,27 @@ __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, ui
             const uint64_t st = fs[i];
             const uint64_t limit = i + 1 < n ? fs[i + 1] : wire_len;
             wsg_recv_info r;
-            const int e = frame_parse(wire, wire_len, st, limit, r);
-            store_info(info + i, r);
+            const int e = frame_parse_b(block, wire_len, st, limit, r);
+            store_info(reinterpret_cast<wsg_recv_info*>(s_info) + t, r);
             const uint64_t pl = e ? st : r.payload_off;
             s_pl[t] = pl;
             s_pe[t] = e ? st : pl + r.len;
             s_key[t] = (e == 0 && r.masked) ? r.key : 0u;
         }
         __syncthreads();
-        if (WSG_LANE_DIAG == 2)   // timing only: the per-frame phase alone
-            continue;
+        {
+            v4u* dst = reinterpret_cast<v4u*>(info + f_lo);
+            for (uint32_t k = t; k < 2 * cnt; k += LANE_THREADS)
+                dst[k] = s_info[k];
+        }
         const uint64_t lo = min(f_lo == 0 ? uint64_t(0) : fs[f_lo], wire_len);
         const uint64_t hi = min(f_lo + cnt < n ? fs[f_lo + cnt] : wire_len, wire_len);
+        if (WSG_LANE_DIAG == 2) {   // timing only: the per-frame phase alone
+            __syncthreads();
+            continue;
+        }
         for (uint64_t p = (lo & ~uint64_t(CHUNK - 1)) + uint64_t(t) * CHUNK; p < hi; p += uint64_t(LANE_THREADS) * CHUNK) {
-            const v4u wv = ld16(wire + p);   // (a 16-B block never crosses a page)
+            const v4u wv = s_wire[p / CHUNK];
             // last frame whose payload starts at or before p (frame 0 if none)
             uint32_t a = 0, b = cnt - 1;
             while (a < b) {
@@ -1620,13 +1664,10 @@ __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, ui
                 if (pl <= p && pe >= p + CHUNK) {   // the chunk lies in this payload
                     const uint32_t kw = key_rot(key, uint32_t(p - pl));
                     m ^= v4u{kw, kw, kw, kw};
-                } else {
-#pragma unroll 1
-                    for (uint32_t k = 0; k < CHUNK; ++k) {
-                        const uint64_t q = p + k;
-                        if (q >= pl && q < pe)
-                            put_byte(m, k, key_byte(key, q - pl));
-                    }
+                } else {   // the payload's bytes of the chunk: [max(pl, p), min(pe, p + 16))
+                    const uint32_t kw = key_rot(key, uint32_t(p - pl));   // (mod 4 also when p < pl)
+                    const uint64_t b0 = pl > p ? pl - p : 0, b1 = pe - p < CHUNK ? pe - p : CHUNK;
+                    m ^= v4u{kw, kw, kw, kw} & (low_bytes(b1) & ~low_bytes(b0));
                 }
             }
             const v4u w = wv ^ m;
@@ -1648,11 +1689,7 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
     __shared__ uint64_t s_a[6];
     __shared__ uint32_t s_op, s_n;
     __shared__ int s_go;
-    __shared__ uint64_t s_u0[LANE_THREADS + 1];   // encode: offsets; decode: payload starts
-    __shared__ uint64_t s_u1[LANE_THREADS];       // decode: payload ends
-    __shared__ uint32_t s_key[LANE_THREADS];
-    __shared__ v4u s_head[LANE_THREADS];
-    __shared__ SmallFrame s_fr[LANE_THREADS];
+    __shared__ v4u s_mem[LANE_LDS / 16];   // the op's staging (lane_decode / lane_encode layouts)
     const uint32_t t = threadIdx.x;
     uint64_t last = 0, seq = 0;
     if (t == 0)
@@ -1688,14 +1725,13 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
         if (!s_go)
             break;
         const uint32_t op = WSG_LANE_DIAG == 1 ? 0u : s_op, n = s_n;   // DIAG 1: answer without the work (timing only)
+        uint8_t* lds = reinterpret_cast<uint8_t*>(s_mem);
         if (op == LANE_DECODE)
             lane_decode(reinterpret_cast<const uint8_t*>(s_a[0]), s_a[1], reinterpret_cast<const uint64_t*>(s_a[2]), n,
-                        reinterpret_cast<uint8_t*>(s_a[3]), reinterpret_cast<wsg_recv_info*>(s_a[4]), s_u0, s_u1,
-                        s_key);
+                        reinterpret_cast<uint8_t*>(s_a[3]), reinterpret_cast<wsg_recv_info*>(s_a[4]), lds);
         else if (op == LANE_ENCODE)
             lane_encode(reinterpret_cast<const uint8_t*>(s_a[0]), reinterpret_cast<const wsg_send_desc*>(s_a[1]), n,
-                        reinterpret_cast<const uint64_t*>(s_a[2]), reinterpret_cast<uint8_t*>(s_a[3]), s_u0, s_head,
-                        s_fr);
+                        reinterpret_cast<const uint64_t*>(s_a[2]), reinterpret_cast<uint8_t*>(s_a[3]), lds);
         __syncthreads();
         if (t == 0) {
             __threadfence_system();   // the request's stores are visible to the host before its answer

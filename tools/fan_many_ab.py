@@ -28,14 +28,16 @@ VAR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 
 def make(spec):
     """spec: "NAME=V,..." environment knobs, or "lib:<variant>" (a build of
     tools/build_variant.sh under cppserver_amd/_build/var)."""
-    if spec.startswith("lib:"):
-        return ca.Codec(0, lib_path=os.path.join(VAR, spec[4:], "libwsg.so"))
+    lib = None
     for k in KNOBS:
         os.environ.pop(k, None)
     for kv in filter(None, spec.split(",")):
+        if kv.startswith("lib:"):
+            lib = os.path.join(VAR, kv[4:], "libwsg.so")
+            continue
         k, _, v = kv.partition("=")
         os.environ[k] = v
-    c = ca.Codec(0)
+    c = ca.Codec(0, lib_path=lib)
     for k in KNOBS:
         os.environ.pop(k, None)
     return c

@@ -37,6 +37,9 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
     size = int(sys.argv[2]) if len(sys.argv) > 2 else 32
     calls = int(sys.argv[3]) if len(sys.argv) > 3 else 3000
+    import torch
+
+    assert torch.cuda.is_available()   # torch's HIP init before the library's first host allocation
     rng = np.random.default_rng(1)
     desc, total = wl.ragged_desc(rng, np.full(n, size))
     pay = ca.pinned_empty(total)
