@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -117,6 +118,12 @@ struct wsg_ctx {
     } lane;
     uint64_t lane_max = 64 << 10;
     uint32_t lane_idle_us = 2000;   // the lane leaves after this long without a request
+    // $WSG_LANE_PROFILE=1: where a lane request's time goes (host: before the
+    // ring, the wait, after the answer; lane: pick-up to staged, to parsed /
+    // heads built, to done, the release fence), printed when the lane stops
+    bool lane_profile = false;
+    double lane_prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t lane_prof_n = 0;
     int wall_khz = 100000;          // constant clock of the lane's idle limit
     // timing of the dominant kernel
     struct EvPair {
@@ -336,6 +343,21 @@ std::vector<wsg_ctx*>& lane_registry()
     return *v;
 }
 
+void lane_report(wsg_ctx* c)
+{
+    if (!c->lane_profile || !c->lane_prof_n)
+        return;
+    const double n = double(c->lane_prof_n);
+    const double* p = c->lane_prof;
+    std::fprintf(stderr,
+                 "WSG_LANE_PROFILE {\"requests\": %llu, \"host_prep_us\": %.2f, \"host_wait_us\": %.2f, "
+                 "\"host_post_us\": %.2f, \"lane_stage_us\": %.2f, \"lane_frames_us\": %.2f, \"lane_rest_us\": %.2f, "
+                 "\"lane_fence_us\": %.2f, \"bell_us\": %.2f}\n",
+                 (unsigned long long)c->lane_prof_n, p[0] / n, p[1] / n, p[2] / n, p[3] / n, p[4] / n, p[5] / n, p[6] / n,
+                 p[7] / n);
+    c->lane_prof_n = 0;
+}
+
 // Ask the lane to leave and wait until it has (its kernel has ended).
 void lane_stop(wsg_ctx* c)
 {
@@ -350,8 +372,10 @@ void lane_stop(wsg_ctx* c)
 void lanes_at_exit()
 {
     std::lock_guard<std::mutex> g(lane_registry_lock());
-    for (wsg_ctx* c : lane_registry())
+    for (wsg_ctx* c : lane_registry()) {
         lane_stop(c);
+        lane_report(c);
+    }
 }
 
 // Launch the lane if it is not running (first use, or it left idle).
@@ -394,14 +418,27 @@ int lane_call(wsg_ctx* c, uint32_t op, uint32_t n, const uint64_t (&a)[6])
     wsg::LaneBell* b = c->lane.bell;
     b->op = op;
     b->n = n;
-    for (int k = 0; k < 6; ++k)
+    for (int k = 0; k < 5; ++k)
         b->a[k] = a[k];
+    b->a[5] = c->lane_profile ? 1 : 0;
     const uint64_t want = ++c->lane.seq;
     __atomic_store_n(&b->seq, want, __ATOMIC_RELEASE);
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t i = 1;; ++i) {
-        if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == want)
+        if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == want) {
+            if (c->lane_profile) {
+                const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+                const double k = 1000.0 / double(c->wall_khz);   // us per tick
+                const uint64_t* v = b->pad0;
+                c->lane_prof[1] += us;
+                c->lane_prof[3] += double(v[1] - v[0]) * k;
+                c->lane_prof[4] += double(v[2] - v[1]) * k;
+                c->lane_prof[5] += double(v[3] - v[2]) * k;
+                c->lane_prof[6] += double(v[4] - v[3]) * k;
+                c->lane_prof[7] += us - double(v[4] - v[0]) * k;
+            }
             return WSG_OK;
+        }
         if ((i & 255) == 0) {
             if (__atomic_load_n(&b->exited, __ATOMIC_ACQUIRE)) {
                 // it left (idle limit) before it saw this request: wait until
@@ -433,6 +470,7 @@ void lane_release(wsg_ctx* c)
     }
     if (!c->lane.broken)
         lane_stop(c);
+    lane_report(c);
     if (c->lane.stream)
         (void)hipStreamDestroy(c->lane.stream);
     if (!c->lane.running)   // (a lane that never answered may still read its doorbell)
@@ -526,6 +564,8 @@ int wsg_create(int device, wsg_ctx** out)
         c->small_avg = std::strtoull(e, nullptr, 10);
     if (const char* e = std::getenv("WSG_LANE_MAX"))   // A/B measurements (tools/echo_size.py, bench_echo)
         c->lane_max = std::strtoull(e, nullptr, 10);
+    if (const char* e = std::getenv("WSG_LANE_PROFILE"))
+        c->lane_profile = *e == '1';
     if (const char* e = std::getenv("WSG_LANE_IDLE_US")) {
         const long v = std::atol(e);
         if (v > 0 && v <= 1000000)
@@ -1111,6 +1151,7 @@ bool strictly_increasing(const uint64_t* v, uint32_t n)
 int decode_host_direct(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start, uint32_t n,
                        uint8_t* out, wsg_recv_info* info)
 {
+    const auto t_in = std::chrono::steady_clock::now();
     wsg_ctx::Slot& sl = c->slots[0];
     if (int rc = slot_reserve(sl, 0, n, false))
         return rc;
@@ -1119,9 +1160,18 @@ int decode_host_direct(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const
         // a few KiB (an echo's read): the resident lane, no launch
         const uint64_t a[6] = {reinterpret_cast<uint64_t>(wire), wire_len, reinterpret_cast<uint64_t>(sl.h_fs),
                                reinterpret_cast<uint64_t>(out), reinterpret_cast<uint64_t>(sl.h_info), 0};
+        const auto t_ring = std::chrono::steady_clock::now();
         if (lane_call(c, wsg::LANE_DECODE, n, a) == WSG_OK) {
+            const auto t_back = std::chrono::steady_clock::now();
             std::memcpy(info, sl.h_info, size_t(n) * sizeof(wsg_recv_info));
-            return host_batch_status(c, wire, wire_len, frame_start, n, info);
+            const int rc = host_batch_status(c, wire, wire_len, frame_start, n, info);
+            if (c->lane_profile) {
+                using us = std::chrono::duration<double, std::micro>;
+                c->lane_prof[0] += us(t_ring - t_in).count();
+                c->lane_prof[2] += us(std::chrono::steady_clock::now() - t_back).count();
+                ++c->lane_prof_n;
+            }
+            return rc;
         }
         // the lane did not answer: the launch path below (from now on always)
     }
@@ -1294,6 +1344,7 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
     try {   // no C++ exception leaves the ABI (host vectors: WSG_ENOMEM)
         if (!c || !wire_off || (n && (!desc || !wire)) || (payload_len && !payload))
             return WSG_EINVAL;
+        const auto t_in = std::chrono::steady_clock::now();   // ($WSG_LANE_PROFILE)
         // frame offsets on the host (the same arithmetic as k_encode_scan_*), so
         // that segments can be cut and copied back without a device round trip
         wire_off[0] = 0;
@@ -1328,8 +1379,14 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
                 std::memcpy(sl.h_fs, wire_off, (size_t(n) + 1) * sizeof(uint64_t));
                 const uint64_t a[6] = {reinterpret_cast<uint64_t>(payload), reinterpret_cast<uint64_t>(sl.h_desc),
                                        reinterpret_cast<uint64_t>(sl.h_fs), reinterpret_cast<uint64_t>(wire), 0, 0};
-                if (lane_call(c, wsg::LANE_ENCODE, n, a) == WSG_OK)
+                const auto t_ring = std::chrono::steady_clock::now();
+                if (lane_call(c, wsg::LANE_ENCODE, n, a) == WSG_OK) {
+                    if (c->lane_profile) {
+                        c->lane_prof[0] += std::chrono::duration<double, std::micro>(t_ring - t_in).count();
+                        ++c->lane_prof_n;
+                    }
                     return WSG_OK;
+                }
             }
             hipStream_t s = c->stream;
             if (int rc = encode_launch(c, s, payload, sl.h_desc, n, wire, wire_off[n], sl.d_woff, sl.enc,

@@ -86,6 +86,9 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_FAN_KSEL
 #define WSG_FAN_KSEL 2   // fan-out period path: a pass's keys by ds_bpermute one pass ahead (2: C4 8.32 vs 8.40 us) or in the pass (0); v_readlane + per-lane selects measured 8.6 us (round 3)
 #endif
+#ifndef WSG_FAN_SLIDE
+#define WSG_FAN_SLIDE 0   // fan-out period path: keys in sliding windows (any passes per wave; A/B)
+#endif
 #ifndef WSG_FAN_UNROLL
 #define WSG_FAN_UNROLL 1   // fan-out period path: passes per loop iteration (A/B)
 #endif
@@ -1566,7 +1569,7 @@ __device__ __forceinline__ void lane_stage(v4u* dst, const uint8_t* __restrict__
 // k_encode_small writes, at the host's offsets.
 __device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload, const wsg_send_desc* __restrict__ desc,
                                             uint32_t n, const uint64_t* __restrict__ wire_off,
-                                            uint8_t* __restrict__ wire, uint8_t* lds)
+                                            uint8_t* __restrict__ wire, uint8_t* lds, uint64_t* ts)
 {
     uint64_t* s_off = reinterpret_cast<uint64_t*>(lds);                             // LANE_THREADS + 1 (+1 pad)
     v4u* s_head = reinterpret_cast<v4u*>(lds + 8 * (LANE_THREADS + 2));
@@ -1583,11 +1586,13 @@ __device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload,
                 s_off[cnt] = wire_off[f_lo + cnt];
         }
         __syncthreads();
+        ts[0] = wall_clock64();
         if (t < cnt) {
             const Desc d = load_desc(reinterpret_cast<const wsg_send_desc*>(s_desc) + t);
             (void)small_head(d, s_head[t], s_fr[t]);
         }
         __syncthreads();
+        ts[1] = wall_clock64();
         if (WSG_LANE_DIAG != 2)   // (DIAG 2, timing only: the per-frame phase alone)
             small_chunks(payload, s_off, s_head, s_fr, cnt, wire, t, LANE_THREADS);
         __syncthreads();   // the group's LDS is reused by the next
@@ -1604,7 +1609,7 @@ __device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload,
 // and error frames' bytes are copied, as k_decode does.
 __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, uint64_t wire_len,
                                             const uint64_t* __restrict__ fs, uint32_t n, uint8_t* out,
-                                            wsg_recv_info* __restrict__ info, uint8_t* lds)
+                                            wsg_recv_info* __restrict__ info, uint8_t* lds, uint64_t* ts)
 {
     v4u* s_wire = reinterpret_cast<v4u*>(lds);
     v4u* s_info = reinterpret_cast<v4u*>(lds + LANE_STAGE);                          // 2 blocks per record
@@ -1615,6 +1620,7 @@ __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, ui
     const uint32_t t = threadIdx.x;
     lane_stage(s_wire, wire, (wire_len + CHUNK - 1) / CHUNK);
     __syncthreads();
+    ts[0] = wall_clock64();   // (thread 0's is the one reported: $WSG_LANE_PROFILE)
     const auto block = [s_wire](uint64_t a) { return s_wire[a / CHUNK]; };
     for (uint32_t f_lo = 0; f_lo < n; f_lo += LANE_THREADS) {
         const uint32_t cnt = min(n - f_lo, LANE_THREADS);
@@ -1631,6 +1637,7 @@ __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, ui
             s_key[t] = (e == 0 && r.masked) ? r.key : 0u;
         }
         __syncthreads();
+        ts[1] = wall_clock64();
         {
             v4u* dst = reinterpret_cast<v4u*>(info + f_lo);
             for (uint32_t k = t; k < 2 * cnt; k += LANE_THREADS)
@@ -1691,7 +1698,8 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
     __shared__ int s_go;
     __shared__ v4u s_mem[LANE_LDS / 16];   // the op's staging (lane_decode / lane_encode layouts)
     const uint32_t t = threadIdx.x;
-    uint64_t last = 0, seq = 0;
+    uint64_t last = 0, seq = 0, t_seen = 0;
+    uint64_t ts[2] = {0, 0};
     if (t == 0)
         last = __hip_atomic_load(&bell->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
     for (;;) {
@@ -1714,6 +1722,7 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
                 __builtin_amdgcn_s_sleep(1);
             }
             if (go) {
+                t_seen = wall_clock64();
                 s_op = __hip_atomic_load(&bell->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 s_n = __hip_atomic_load(&bell->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 for (int k = 0; k < 6; ++k)
@@ -1728,13 +1737,20 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
         uint8_t* lds = reinterpret_cast<uint8_t*>(s_mem);
         if (op == LANE_DECODE)
             lane_decode(reinterpret_cast<const uint8_t*>(s_a[0]), s_a[1], reinterpret_cast<const uint64_t*>(s_a[2]), n,
-                        reinterpret_cast<uint8_t*>(s_a[3]), reinterpret_cast<wsg_recv_info*>(s_a[4]), lds);
+                        reinterpret_cast<uint8_t*>(s_a[3]), reinterpret_cast<wsg_recv_info*>(s_a[4]), lds, ts);
         else if (op == LANE_ENCODE)
             lane_encode(reinterpret_cast<const uint8_t*>(s_a[0]), reinterpret_cast<const wsg_send_desc*>(s_a[1]), n,
-                        reinterpret_cast<const uint64_t*>(s_a[2]), reinterpret_cast<uint8_t*>(s_a[3]), lds);
+                        reinterpret_cast<const uint64_t*>(s_a[2]), reinterpret_cast<uint8_t*>(s_a[3]), lds, ts);
         __syncthreads();
         if (t == 0) {
+            const uint64_t t_work = wall_clock64();
             __threadfence_system();   // the request's stores are visible to the host before its answer
+            if (s_a[5]) {   // $WSG_LANE_PROFILE: the request's phases on the constant clock
+                const uint64_t t_fenced = wall_clock64();
+                const uint64_t v[5] = {t_seen, ts[0], ts[1], t_work, t_fenced};
+                for (int k = 0; k < 5; ++k)
+                    __hip_atomic_store(&bell->pad0[k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             __hip_atomic_store(&bell->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             last = seq;
         }
@@ -2012,14 +2028,28 @@ __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restric
     // payload loads, so the two arrive together: the kernel is short (41 MB
     // at C4), and a second dependent memory round trip before the first
     // store was a visible share of it
-    uint32_t kv[WSG_FAN_KV];
+    // WSG_FAN_SLIDE: the keys come in windows of PW passes (kv: the current
+    // window, kv_nx: the next, loaded a window ahead), so a wave may make any
+    // number of passes (fewer, longer-lived waves: the write stream of
+    // tools/membench.hip's row pattern at 4 waves/CU)
+    constexpr uint32_t PW = 64 * WSG_FAN_KV / KW;   // passes per key window
+    auto load_window = [&](uint32_t w0, uint32_t (&dst)[WSG_FAN_KV]) {
 #pragma unroll
-    for (int h = 0; h < WSG_FAN_KV; ++h) {
-        const uint32_t s = uint32_t(h) * 64 + lane;
-        const uint64_t it = s / KW;
-        const uint64_t idx = uint64_t(P) * (m0 + it * dm) + (s % KW);
-        kv[h] = (WSG_DIAG_FAN & 32) ? uint32_t(idx) : (row0 + it * rstep < chunks && idx < k) ? keys[idx] : 0u;
-    }
+        for (int h = 0; h < WSG_FAN_KV; ++h) {
+            const uint32_t s = uint32_t(h) * 64 + lane;
+            const uint64_t it = uint64_t(w0) + s / KW;
+            const uint64_t idx = uint64_t(P) * (m0 + it * dm) + (s % KW);
+            dst[h] = (WSG_DIAG_FAN & 32) ? uint32_t(idx) : (row0 + it * rstep < chunks && idx < k) ? keys[idx] : 0u;
+        }
+    };
+    uint32_t kv[WSG_FAN_KV], kv_nx[WSG_FAN_KV];
+    load_window(0, kv);
+    if (WSG_FAN_SLIDE)
+        load_window(PW, kv_nx);
+    else
+        for (int h = 0; h < WSG_FAN_KV; ++h)
+            kv_nx[h] = 0;
+    uint32_t w0 = 0;   // first pass of the window in kv
 
     // template of chunk j: its frame-a bytes, and the next frame's from byte
     // `split` on (the first 16 bytes of a frame: the same for every lane)
@@ -2080,11 +2110,19 @@ __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restric
     // The keys of pass `it` for this lane: frame a's (slot ia) and, where a
     // frame starts inside the lane's chunk, frame b's (slot ia + 1).
     auto pass_keys = [&](uint32_t it, uint32_t& ka, uint32_t& kb, bool want_b) {
-        const uint32_t slot = it * KW;                      // wave-uniform; KW divides 64
+        uint32_t slot = (it - w0) * KW;                     // wave-uniform; KW divides 64
         uint32_t kreg = kv[0];
+        if (WSG_FAN_SLIDE && slot >= 64 * WSG_FAN_KV) {    // the next window's (one pass ahead)
+            slot -= 64 * WSG_FAN_KV;
+            kreg = kv_nx[0];
 #pragma unroll
-        for (int h = 1; h < WSG_FAN_KV; ++h)
-            kreg = (slot >> 6) == uint32_t(h) ? kv[h] : kreg;
+            for (int h = 1; h < WSG_FAN_KV; ++h)
+                kreg = (slot >> 6) == uint32_t(h) ? kv_nx[h] : kreg;
+        } else {
+#pragma unroll
+            for (int h = 1; h < WSG_FAN_KV; ++h)
+                kreg = (slot >> 6) == uint32_t(h) ? kv[h] : kreg;
+        }
         const uint32_t sb = (slot & 63) * 4;
         ka = __builtin_amdgcn_ds_bpermute(int(addr + sb), int(kreg));
         kb = want_b ? __builtin_amdgcn_ds_bpermute(int(addr + sb + 4), int(kreg)) : 0u;
@@ -2121,6 +2159,13 @@ __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restric
 #pragma unroll WSG_FAN_UNROLL
         for (uint32_t it = 0; it < n_full; ++it) {
             const v4u w = word(it);
+            if (WSG_FAN_SLIDE && it + 1 - w0 == PW) {   // (wave-uniform) the next window takes over
+#pragma unroll
+                for (int h = 0; h < WSG_FAN_KV; ++h)
+                    kv[h] = kv_nx[h];
+                w0 += PW;
+                load_window(w0 + PW, kv_nx);
+            }
             if ((WSG_DIAG_FAN & 64) && (w[0] & w[1] & w[2] & w[3]) != 0xA5C3E1F7u) {
                 // diagnostic: the computation without its stores
             } else if (WSG_FAN_SC1) {
@@ -2276,7 +2321,8 @@ bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, int wpb, con
     const uint64_t rows = (chunks + 63) / 64;
     uint64_t mult = std::max<uint64_t>(1, (uint64_t(cus) * waves_per_cu + Q / 2) / Q);
     mult = std::min(mult, (rows + Q - 1) / Q);                                                 // no idle waves
-    mult = std::max(mult, (chunks + Q * 64 * max_passes - 1) / (Q * 64 * max_passes));   // one key load
+    if (!WSG_FAN_SLIDE)   // every pass's keys in one load per lane
+        mult = std::max(mult, (chunks + Q * 64 * max_passes - 1) / (Q * 64 * max_passes));
     const uint64_t W = Q * mult;
     if (W > (1u << 22))
         return false;
