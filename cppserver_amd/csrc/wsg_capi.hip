@@ -287,6 +287,19 @@ bool in_alloc(const void* p, uint64_t bytes)
 
 namespace {
 
+// Page-locked host memory the kernels read and write in place (the session
+// batches' buffers, the direct paths' tables): coherent (fine-grained)
+// when $WSG_HOST_COHERENT=1, else the runtime's default (A/B: the lane's
+// PCIe reads of it, tools/lane_ab.py).
+unsigned host_alloc_flags()
+{
+    static const unsigned f = [] {
+        const char* e = std::getenv("WSG_HOST_COHERENT");
+        return (e && *e == '1') ? unsigned(hipHostMallocCoherent | hipHostMallocMapped) : unsigned(hipHostMallocDefault);
+    }();
+    return f;
+}
+
 // The blocks wsg_host_alloc made (page-locked, mapped at the same address on
 // the device): a host batch in one of them (the session batches' buffers
 // always are) is recognised without a runtime query, whose few us per
@@ -1047,8 +1060,8 @@ int slot_reserve(wsg_ctx::Slot& sl, uint64_t bytes, uint64_t frames, bool need_h
         sl.frames_cap = 0;
         if (hipMalloc(&sl.d_fs, frames * sizeof(uint64_t)) != hipSuccess ||
             hipMalloc(&sl.d_info, frames * sizeof(wsg_recv_info)) != hipSuccess ||
-            hipHostMalloc(&sl.h_fs, frames * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc(&sl.h_info, frames * sizeof(wsg_recv_info), hipHostMallocDefault) != hipSuccess)
+            hipHostMalloc(&sl.h_fs, frames * sizeof(uint64_t), host_alloc_flags()) != hipSuccess ||
+            hipHostMalloc(&sl.h_info, frames * sizeof(wsg_recv_info), host_alloc_flags()) != hipSuccess)
             return WSG_ENOMEM;
         sl.frames_cap = frames;
     }
@@ -1091,7 +1104,7 @@ int wsg_host_alloc(size_t bytes, void** out)
     if (!out)
         return WSG_EINVAL;
     *out = nullptr;
-    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc(out, bytes ? bytes : 1, host_alloc_flags()) != hipSuccess)
         return WSG_ENOMEM;
     host_blocks_add(*out, bytes ? bytes : 1);
     return WSG_OK;
@@ -1315,7 +1328,7 @@ int slot_reserve_enc(wsg_ctx::Slot& sl, uint64_t payload_bytes, uint64_t wire_by
             (void)hipHostFree(sl.h_desc);
         sl.h_desc = nullptr;
         sl.h_desc_cap = 0;
-        if (hipHostMalloc(&sl.h_desc, frames * sizeof(wsg_send_desc), hipHostMallocDefault) != hipSuccess)
+        if (hipHostMalloc(&sl.h_desc, frames * sizeof(wsg_send_desc), host_alloc_flags()) != hipSuccess)
             return WSG_ENOMEM;
         sl.h_desc_cap = frames;
     }

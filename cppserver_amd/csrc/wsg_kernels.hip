@@ -1716,23 +1716,36 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
                     go = 1;
                     break;
                 }
-                if (__hip_atomic_load(&bell->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                    wall_clock64() - t0 > idle_ticks)
+                // (stop and the clock every 16th poll: each PCIe read is a
+                // round trip the next request would wait behind)
+                if ((it & 15) == 15 &&
+                    (__hip_atomic_load(&bell->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                     wall_clock64() - t0 > idle_ticks))
                     break;
                 __builtin_amdgcn_s_sleep(1);
             }
-            if (go) {
+            if (go)
                 t_seen = wall_clock64();
-                s_op = __hip_atomic_load(&bell->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                s_n = __hip_atomic_load(&bell->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                for (int k = 0; k < 6; ++k)
-                    s_a[k] = __hip_atomic_load(&bell->a[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
             s_go = go;
         }
         __syncthreads();
         if (!s_go)
             break;
+        // the request's words (op | n, a[0..5]) in one round trip: a lane
+        // each (one after another from thread 0 they were seven PCIe reads,
+        // ~10 us before any work, $WSG_LANE_PROFILE)
+        if (t < 7) {
+            const uint64_t* words = reinterpret_cast<const uint64_t*>(&bell->op);
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);   // (after thread 0's sight of seq: the barrier above)
+            const uint64_t v = __hip_atomic_load(words + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (t == 0) {
+                s_op = uint32_t(v);
+                s_n = uint32_t(v >> 32);
+            } else {
+                s_a[t - 1] = v;
+            }
+        }
+        __syncthreads();
         const uint32_t op = WSG_LANE_DIAG == 1 ? 0u : s_op, n = s_n;   // DIAG 1: answer without the work (timing only)
         uint8_t* lds = reinterpret_cast<uint8_t*>(s_mem);
         if (op == LANE_DECODE)
