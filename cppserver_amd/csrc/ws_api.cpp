@@ -157,8 +157,7 @@ void WSClient::SetSendBatch(WSSendBatch* batch)
     WSSendBatch* old;
     {
         std::scoped_lock locker(_ws_send_lock);
-        old = _tx_batch;
-        _tx_batch = batch;
+        old = _tx_batch.exchange(batch, std::memory_order_acq_rel);
     }
     // not under the send lock: Forget may wait for a flush on another thread
     // whose deliveries take session send locks (a multicast)
@@ -169,8 +168,8 @@ void WSClient::SetSendBatch(WSSendBatch* batch)
 size_t WSClient::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status,
                            const CppCommon::Timespan* timeout)
 {
-    if (_tx_batch)
-        _tx_batch->Flush();   // earlier async frames go first
+    if (WSSendBatch* b = _tx_batch.load(std::memory_order_acquire))
+        b->Flush();   // earlier async frames go first
     else if (BatchScope::Active())
         BatchScope::Send().Flush();
     std::scoped_lock locker(_ws_send_lock);
@@ -181,10 +180,19 @@ size_t WSClient::SendFrame(uint8_t opcode, const void* buffer, size_t size, int 
 
 bool WSClient::SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status)
 {
+    if (!_tx_batch.load(std::memory_order_acquire) && BatchScope::Active()) {
+        // the thread's own scope: nothing of this connection but its key is
+        // touched, and the scope's queue has its own lock
+        BatchScope::Send().Queue(_transport, send_key(), opcode, true, buffer, size, status);
+        BatchScope::CheckLimits();
+        return true;
+    }
     {
         std::scoped_lock locker(_ws_send_lock);
-        if (_tx_batch) {
-            _tx_batch->Queue(_transport, send_key(), opcode, true, buffer, size, status);
+        if (WSSendBatch* b = _tx_batch.load(std::memory_order_relaxed)) {
+            // an explicit batch: queued under the send lock, so that once
+            // SetSendBatch has swapped it out no thread is still queueing into it
+            b->Queue(_transport, send_key(), opcode, true, buffer, size, status);
             return true;
         }
         if (!BatchScope::Active()) {
@@ -338,8 +346,7 @@ void WSSession::SetSendBatch(WSSendBatch* batch)
     WSSendBatch* old;
     {
         std::scoped_lock locker(_ws_send_lock);
-        old = _tx_batch;
-        _tx_batch = batch;
+        old = _tx_batch.exchange(batch, std::memory_order_acq_rel);
     }
     // not under the send lock: Forget may wait for a flush on another thread
     // whose deliveries take session send locks (a multicast)
@@ -350,8 +357,8 @@ void WSSession::SetSendBatch(WSSendBatch* batch)
 size_t WSSession::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status,
                             const CppCommon::Timespan* timeout)
 {
-    if (_tx_batch)
-        _tx_batch->Flush();   // earlier async frames go first
+    if (WSSendBatch* b = _tx_batch.load(std::memory_order_acquire))
+        b->Flush();   // earlier async frames go first
     else if (BatchScope::Active())
         BatchScope::Send().Flush();
     std::scoped_lock locker(_ws_send_lock);
@@ -362,10 +369,19 @@ size_t WSSession::SendFrame(uint8_t opcode, const void* buffer, size_t size, int
 
 bool WSSession::SendFrameAsync(uint8_t opcode, const void* buffer, size_t size, int status)
 {
+    if (!_tx_batch.load(std::memory_order_acquire) && BatchScope::Active()) {
+        // the thread's own scope: nothing of this connection but its key is
+        // touched, and the scope's queue has its own lock
+        BatchScope::Send().Queue(_transport, send_key(), opcode, false, buffer, size, status);
+        BatchScope::CheckLimits();
+        return true;
+    }
     {
         std::scoped_lock locker(_ws_send_lock);
-        if (_tx_batch) {
-            _tx_batch->Queue(_transport, send_key(), opcode, false, buffer, size, status);
+        if (WSSendBatch* b = _tx_batch.load(std::memory_order_relaxed)) {
+            // an explicit batch: queued under the send lock, so that once
+            // SetSendBatch has swapped it out no thread is still queueing into it
+            b->Queue(_transport, send_key(), opcode, false, buffer, size, status);
             return true;
         }
         if (!BatchScope::Active()) {

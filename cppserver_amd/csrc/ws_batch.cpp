@@ -9,6 +9,7 @@
 #include "server/ws/ws_batch.h"
 #include "server/ws/ws_transport.h"
 #include "ws_session_impl.h"
+#include "wsg_frame.h"
 
 #include <algorithm>
 #include <condition_variable>
@@ -299,14 +300,20 @@ size_t WSReceiveBatch::Flush()
     if (!keyed)
         payload_base = b.wire.p;
     size_t delivered = 0;
+    const void* announced = nullptr;
     // b.recs is written only by this thread (its callbacks' Forget); other
     // threads' Forget()s are applied here, between two records
     for (size_t r = 0; r < b.recs.size(); ++r) {
-        // announce the connection, then look for Forgets (see Forget)
-        _busy.store(b.recs[r].ws, std::memory_order_seq_cst);
-        if (_waiters.load(std::memory_order_seq_cst)) {
-            std::scoped_lock locker(_lock);   // a Forget waiting for the previous connection may go
-            _busy_cv.notify_all();
+        // announce the connection, then look for Forgets (see Forget).  Only
+        // this thread writes _busy, so while the records stay on one
+        // connection it already holds that connection: no store, no wake-up
+        if (b.recs[r].ws != announced) {
+            announced = b.recs[r].ws;
+            _busy.store(announced, std::memory_order_seq_cst);
+            if (_waiters.load(std::memory_order_seq_cst)) {
+                std::scoped_lock locker(_lock);   // a Forget waiting for the previous connection may go
+                _busy_cv.notify_all();
+            }
         }
         if (_has_pending.load(std::memory_order_seq_cst)) {
             std::scoped_lock locker(_lock);
@@ -508,7 +515,8 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
     for (uint32_t i = 0; i < n; ++i) {
         const wsg_send_desc& d = b.desc[i];
         _wire_off[i] = total;
-        total += wsg_frame_size(d.opcode, d.mask, d.len, d.status);
+        const wsg::SendGeom g = wsg::send_geom(d.opcode, d.mask != 0, d.len, d.status);   // = wsg_frame_size
+        total += g.hdr + g.body;
         keyed = keyed || d.key != 0;
     }
     _wire_off[n] = total;
@@ -527,15 +535,15 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
         for (uint32_t i = 0; i < n; ++i) {
             const wsg_send_desc& d = b.desc[i];
             uint8_t* f = _wire.p + _wire_off[i];
-            const uint64_t size = _wire_off[i + 1] - _wire_off[i];
-            const int hdr = wsg_header_pack(d.opcode, d.mask, d.len, d.status, 0, f);
-            const uint64_t prefix = size - uint64_t(hdr) - d.len;
-            if (prefix) {
-                f[hdr] = uint8_t((d.status >> 8) & 0xFF);
-                f[hdr + 1] = uint8_t(d.status & 0xFF);
+            const wsg::SendGeom g = wsg::send_geom(d.opcode, d.mask != 0, d.len, d.status);
+            for (uint32_t r = 0; r < g.hdr; ++r)   // = wsg_header_pack with key 0
+                f[r] = wsg::header_byte(d.opcode, d.mask != 0, g.body, 0, r);
+            if (g.prefix) {
+                f[g.hdr] = uint8_t((d.status >> 8) & 0xFF);
+                f[g.hdr + 1] = uint8_t(d.status & 0xFF);
             }
             if (d.len)
-                std::memcpy(f + hdr + prefix, b.payload.p + d.src_off, d.len);
+                std::memcpy(f + g.hdr + g.prefix, b.payload.p + d.src_off, d.len);
         }
     }
     if (rc != WSG_OK) {
@@ -562,19 +570,23 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
         check(rc, "wsg_encode_batch_host");
     }
     size_t sent = 0;
+    const void* announced = nullptr;
     // b.recs is written only by this thread (its callbacks' Forget); other
-    // threads' Forget()s are applied here, between two frames
-    for (uint32_t i = 0; i < n; ++i) {
+    // threads' Forget()s are applied here, between two hand-outs
+    for (uint32_t i = 0; i < n;) {
         const uint8_t* f = _wire.p + _wire_off[i];
-        const size_t len = size_t(_wire_off[i + 1] - _wire_off[i]);
         {
+            // announced only when the target changes (see WSReceiveBatch::Flush)
             const Rec& next = b.recs[i];
-            _busy.store(next.transport ? static_cast<const void*>(next.transport) : next.tag,
-                        std::memory_order_seq_cst);
-        }
-        if (_waiters.load(std::memory_order_seq_cst)) {
-            std::scoped_lock locker(_lock);
-            _busy_cv.notify_all();
+            const void* target = next.transport ? static_cast<const void*>(next.transport) : next.tag;
+            if (target != announced) {
+                announced = target;
+                _busy.store(target, std::memory_order_seq_cst);
+                if (_waiters.load(std::memory_order_seq_cst)) {
+                    std::scoped_lock locker(_lock);
+                    _busy_cv.notify_all();
+                }
+            }
         }
         if (_has_pending.load(std::memory_order_seq_cst)) {
             std::scoped_lock locker(_lock);
@@ -582,15 +594,25 @@ size_t WSSendBatch::Flush(Sink sink, void* user)
         }
         const Rec& rec = b.recs[i];   // written by this thread only (ApplyPending above)
         if (rec.transport) {
-            rec.transport->SendAsync(f, len);
-            ++sent;
-        } else if (rec.deliver) {
+            // a run of frames for one transport lies contiguous in _wire: one
+            // SendAsync hands the transport the same bytes in the same order
+            uint32_t j = i + 1;
+            while (j < n && b.recs[j].transport == rec.transport)
+                ++j;
+            rec.transport->SendAsync(f, size_t(_wire_off[j] - _wire_off[i]));
+            sent += j - i;
+            i = j;
+            continue;
+        }
+        const size_t len = size_t(_wire_off[i + 1] - _wire_off[i]);
+        if (rec.deliver) {
             (*rec.deliver)(f, len);
             ++sent;
         } else if (rec.tag && sink) {
             sink(user, rec.tag, f, len);
             ++sent;
         }
+        ++i;
     }
     return sent;
 }

@@ -5,12 +5,18 @@
 // :309-386 (header half of PrepareReceiveFrame).
 #pragma once
 
-#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "wsg_capi.h"
 
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
 #define WSG_HD __host__ __device__ __forceinline__
+#else
+// the host-only WebSocket classes (and their g++ sanitizer builds) use the
+// same arithmetic without the HIP headers
+#define WSG_HD inline
+#endif
 
 namespace wsg {
 

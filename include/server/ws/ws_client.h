@@ -117,7 +117,7 @@ protected:
 private:
     std::string _http_buf;   // upgrade response bytes until its header block is complete
     std::atomic<WSReceiveBatch*> _rx_batch{nullptr};   // swapped by SetReceiveBatch, read by the IO thread
-    WSSendBatch* _tx_batch{nullptr};
+    std::atomic<WSSendBatch*> _tx_batch{nullptr};
     void ResetBuffers();
     void RouteFrames(const void* buffer, size_t size);
     size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0,

@@ -449,6 +449,51 @@ static void test_batched_send()
     server.EnableBatchSend(false);
 }
 
+// A flush hands each transport its frames in runs: consecutive frames for one
+// transport lie contiguous in the wire and go out in one SendAsync; the bytes
+// and their order are exactly the per-frame hand-outs'.
+static void test_send_batch_runs()
+{
+    struct Counting : Transport {
+        std::vector<std::vector<uint8_t>> calls;
+        size_t Send(const void* b, size_t n) override { return SendAsync(b, n) ? n : 0; }
+        bool SendAsync(const void* b, size_t n) override
+        {
+            calls.emplace_back(static_cast<const uint8_t*>(b), static_cast<const uint8_t*>(b) + n);
+            return true;
+        }
+        size_t Receive(void*, size_t) override { return 0; }
+        bool Disconnect() override { return true; }
+        bool IsConnected() const override { return true; }
+    } a, b;
+    WSSendBatch batch;
+    const std::vector<std::pair<Counting*, std::string>> order = {
+        {&a, "a1"}, {&a, "a2"}, {&a, std::string(300, 'x')}, {&b, "b1"}, {&a, "a3"}, {&b, "b2"}, {&b, ""}};
+    std::vector<uint8_t> want_a, want_b;
+    for (const auto& [t, text] : order) {
+        batch.Queue(*t, 0, WSG_FIN | WSG_BINARY, false, text.data(), text.size(), 0);
+        std::vector<uint8_t>& w = t == &a ? want_a : want_b;
+        w.push_back(WSG_FIN | WSG_BINARY);
+        if (text.size() < 126) {
+            w.push_back(uint8_t(text.size()));
+        } else {
+            w.push_back(126);
+            w.push_back(uint8_t(text.size() >> 8));
+            w.push_back(uint8_t(text.size()));
+        }
+        w.insert(w.end(), text.begin(), text.end());
+    }
+    CHECK(batch.Flush() == order.size());
+    CHECK(a.calls.size() == 2 && b.calls.size() == 2);   // runs: a a a | b | a | b b
+    std::vector<uint8_t> got_a, got_b;
+    for (auto& c : a.calls)
+        got_a.insert(got_a.end(), c.begin(), c.end());
+    for (auto& c : b.calls)
+        got_b.insert(got_b.end(), c.begin(), c.end());
+    CHECK(got_a == want_a && got_b == want_b);
+    CHECK(a.calls.size() == 2 && a.calls[1].size() == 4);   // "a3" alone: its own hand-out
+}
+
 // Automatic batching (ws_batch.h BatchScope): the drop-in path, no batch
 // set up by the user.  Sends inside a tick leave in one encode pass at its
 // end; a read's frames are unmasked in one pass and the echoes they trigger
@@ -754,6 +799,7 @@ int main()
         test_batched_server_receive({0, 0, 0});
         unsetenv("WSG_HOST_MULTI_SHARE");
         test_batched_send();
+        test_send_batch_runs();
         test_auto_batch_echo();
         test_multicast_tick();
         test_batch_threads();
