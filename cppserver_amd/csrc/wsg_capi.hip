@@ -106,8 +106,9 @@ struct wsg_ctx {
     // stream per slot instead, the earlier design, kept for A/B runs)
     hipStream_t s_h2d = nullptr, s_kern = nullptr, s_d2h = nullptr;
     // the host lane (wsg_internal.h): page-locked host batches of at most
-    // lane_max wire bytes go to a resident one-workgroup kernel through a
-    // doorbell instead of a launch + synchronize ($WSG_LANE_MAX, 0 = never)
+    // lane_max wire bytes go to a resident kernel of lane_wgs workgroups
+    // through a doorbell instead of a launch + synchronize ($WSG_LANE_MAX,
+    // 0 = never; $WSG_LANE_WGS)
     struct Lane {
         wsg::LaneBell* bell = nullptr;   // page-locked, coherent
         hipStream_t stream = nullptr;
@@ -115,9 +116,13 @@ struct wsg_ctx {
         bool broken = false;             // did not answer: the launch paths from now on
         uint64_t seq = 0;
         uint64_t launches = 0;           // kernel launches of the lane (wsg_lane_stats)
+        uint32_t gen = 0;                // the running launch's number (exited[] holds it when it leaves)
     } lane;
     uint64_t lane_max = 64 << 10;
+    uint32_t lane_wgs = 8;          // workgroups (CUs) sharing a request's reads and writes
+    bool tables_in_place = true;    // the direct paths use tables in wsg_host_alloc blocks in place ($WSG_TABLES_IN_PLACE, A/B)
     uint32_t lane_idle_us = 2000;   // the lane leaves after this long without a request
+    uint32_t lane_reqs = 256;       // ... and after every lane_reqs-th request ($WSG_LANE_REQS)
     // $WSG_LANE_PROFILE=1: where a lane request's time goes (host: before the
     // ring, the wait, after the answer; lane: pick-up to staged, to parsed /
     // heads built, to done, the release fence), printed when the lane stops
@@ -325,7 +330,7 @@ void host_blocks_remove(const void* p)
     std::lock_guard<std::mutex> g(host_blocks_lock());
     host_blocks().erase(reinterpret_cast<uintptr_t>(p));
 }
-bool in_host_block(const void* p)
+bool in_host_block(const void* p, uint64_t bytes = 1)
 {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     std::lock_guard<std::mutex> g(host_blocks_lock());
@@ -334,7 +339,7 @@ bool in_host_block(const void* p)
     if (it == m.begin())
         return false;
     --it;
-    return a - it->first < it->second;
+    return a - it->first < it->second && bytes <= it->second - (a - it->first);
 }
 
 } // namespace
@@ -365,16 +370,17 @@ void lane_report(wsg_ctx* c)
     std::fprintf(stderr,
                  "WSG_LANE_PROFILE {\"requests\": %llu, \"host_prep_us\": %.2f, \"host_wait_us\": %.2f, "
                  "\"host_post_us\": %.2f, \"lane_stage_us\": %.2f, \"lane_frames_us\": %.2f, \"lane_rest_us\": %.2f, "
-                 "\"lane_fence_us\": %.2f, \"bell_us\": %.2f}\n",
+                 "\"lane_fence_us\": %.2f, \"bell_us\": %.2f, \"launches\": %llu}\n",
                  (unsigned long long)c->lane_prof_n, p[0] / n, p[1] / n, p[2] / n, p[3] / n, p[4] / n, p[5] / n, p[6] / n,
-                 p[7] / n);
+                 p[7] / n, (unsigned long long)c->lane.launches);
     c->lane_prof_n = 0;
 }
 
-// Ask the lane to leave and wait until it has (its kernel has ended).
+// Ask the lane to leave and wait until it has (its kernel has ended; a
+// launch that ended after its last request may still be finishing).
 void lane_stop(wsg_ctx* c)
 {
-    if (!c->lane.running)
+    if (!c->lane.bell || !c->lane.launches)
         return;
     (void)hipSetDevice(c->device);
     __atomic_store_n(&c->lane.bell->stop, 1u, __ATOMIC_RELEASE);
@@ -411,38 +417,66 @@ int lane_start(wsg_ctx* c)
         return WSG_OK;
     wsg::LaneBell* b = c->lane.bell;
     b->stop = 0;
-    b->exited = 0;
+    // (queued behind the previous launch on the lane's stream when that one
+    // is still ending: it starts from each workgroup's `done`)
     const uint64_t idle = uint64_t(c->lane_idle_us) * uint64_t(c->wall_khz) / 1000u;
-    if (wsg::launch_lane(c->lane.stream, b, idle) != hipSuccess)
+    if (++c->lane.gen == 0)
+        ++c->lane.gen;
+    if (wsg::launch_lane(c->lane.stream, b, c->lane_wgs, idle, c->lane.gen, c->lane_reqs) != hipSuccess)
         return WSG_EHIP;
     c->lane.running = true;
     ++c->lane.launches;
     return WSG_OK;
 }
 
-// One request on the lane; returns when it is answered.  WSG_EHIP when the
-// lane does not answer within seconds (it is then not used again).
-int lane_call(wsg_ctx* c, uint32_t op, uint32_t n, const uint64_t (&a)[6])
+// Frames per group for a request of n frames: the workgroups share the
+// frames evenly, a group at most LANE_THREADS frames, and no workgroup takes
+// more than LANE_GROUPS_PER_WG groups (n <= lane_max_frames).
+uint32_t lane_max_frames(const wsg_ctx* c)
 {
-    if (c->lane.broken)
-        return WSG_EHIP;
-    if (int rc = lane_start(c))
-        return rc;
+    return std::min<uint32_t>(wsg::LANE_GROUPS_MAX, c->lane_wgs * wsg::LANE_GROUPS_PER_WG) * wsg::LANE_THREADS;
+}
+uint32_t lane_group_size(const wsg_ctx* c, uint32_t n)
+{
+    uint32_t G = (n + c->lane_wgs - 1) / c->lane_wgs;
+    G = std::max<uint32_t>(G, (n + c->lane_wgs * wsg::LANE_GROUPS_PER_WG - 1) / (c->lane_wgs * wsg::LANE_GROUPS_PER_WG));
+    G = std::max<uint32_t>(G, (n + wsg::LANE_GROUPS_MAX - 1) / wsg::LANE_GROUPS_MAX);
+    return std::max<uint32_t>(1, std::min<uint32_t>(G, wsg::LANE_THREADS));
+}
+
+// One request on the lane (the group ranges already in bell->grp); returns
+// when every workgroup has answered.  WSG_EHIP when the lane does not answer
+// within seconds (it is then not used again).
+int lane_call(wsg_ctx* c, uint32_t op, uint32_t n, uint32_t G, const uint64_t (&a)[6])
+{
     wsg::LaneBell* b = c->lane.bell;
-    b->op = op;
-    b->n = n;
-    for (int k = 0; k < 5; ++k)
-        b->a[k] = a[k];
-    b->a[5] = c->lane_profile ? 1 : 0;
     const uint64_t want = ++c->lane.seq;
-    __atomic_store_n(&b->seq, want, __ATOMIC_RELEASE);
+    // every unit a workgroup reads gets this request's tag, each after its
+    // value (x86 stores are seen in program order; the release stores keep
+    // the compiler's order): the group ranges (the caller's values), then
+    // the request words, the first one last (the lane polls its tag)
+    for (uint32_t k = 0; k < wsg::LANE_GROUPS_MAX; ++k)
+        for (int h = 0; h < 2; ++h)
+            __atomic_store_n(&b->grp[k][h].tag, want, __ATOMIC_RELEASE);
+    uint64_t w[wsg::LANE_WORDS] = {uint64_t(op) | (uint64_t(n) << 32), a[0], a[1], a[2], a[3], a[4], a[5],
+                                   uint64_t(G) | (uint64_t(c->lane_profile ? 1 : 0) << 32)};
+    for (uint32_t k = wsg::LANE_WORDS; k-- > 0;) {   // w[0] last: the lane polls its tag
+        b->w[k].v = w[k];
+        __atomic_store_n(&b->w[k].tag, want, __ATOMIC_RELEASE);
+    }
     const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t nw = c->lane_wgs;
+    uint32_t g = 0;   // workgroups [0, g) have answered
     for (uint64_t i = 1;; ++i) {
-        if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == want) {
+        while (g < nw && __atomic_load_n(&b->done[g], __ATOMIC_ACQUIRE) == want)
+            ++g;
+        if (g == nw) {
+            if (want % c->lane_reqs == 0)
+                c->lane.running = false;   // this launch ends after this request: the next call launches again
             if (c->lane_profile) {
                 const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
                 const double k = 1000.0 / double(c->wall_khz);   // us per tick
-                const uint64_t* v = b->pad0;
+                const uint64_t* v = b->prof;
                 c->lane_prof[1] += us;
                 c->lane_prof[3] += double(v[1] - v[0]) * k;
                 c->lane_prof[4] += double(v[2] - v[1]) * k;
@@ -453,11 +487,15 @@ int lane_call(wsg_ctx* c, uint32_t op, uint32_t n, const uint64_t (&a)[6])
             return WSG_OK;
         }
         if ((i & 255) == 0) {
-            if (__atomic_load_n(&b->exited, __ATOMIC_ACQUIRE)) {
-                // it left (idle limit) before it saw this request: wait until
-                // its kernel has ended, then launch it again; the new one
-                // starts from `done` and takes the request
-                (void)hipStreamSynchronize(c->lane.stream);
+            bool left = false;
+            for (uint32_t k = 0; k < nw; ++k)
+                left = left || __atomic_load_n(&b->exited[k], __ATOMIC_ACQUIRE) == c->lane.gen;
+            if (left) {
+                // a workgroup of the running launch left (idle limit) before
+                // it saw this request: launch again, behind it on the
+                // stream (its other workgroups leave idle too); each new
+                // workgroup starts from its own `done` and takes its share
+                // if it is still owed
                 c->lane.running = false;
                 if (int rc = lane_start(c))
                     return rc;
@@ -470,6 +508,15 @@ int lane_call(wsg_ctx* c, uint32_t op, uint32_t n, const uint64_t (&a)[6])
         }
         __builtin_ia32_pause();
     }
+}
+
+// The lane for a request, launched if it is not running; nullptr when it
+// cannot be used (it did not answer before, or its launch failed).
+wsg::LaneBell* lane_ready(wsg_ctx* c)
+{
+    if (c->lane.broken || lane_start(c) != WSG_OK)
+        return nullptr;
+    return c->lane.bell;
 }
 
 void lane_release(wsg_ctx* c)
@@ -579,6 +626,18 @@ int wsg_create(int device, wsg_ctx** out)
         c->lane_max = std::strtoull(e, nullptr, 10);
     if (const char* e = std::getenv("WSG_LANE_PROFILE"))
         c->lane_profile = *e == '1';
+    if (const char* e = std::getenv("WSG_LANE_REQS")) {
+        const long v = std::atol(e);
+        if (v >= 1 && v <= (1l << 30))
+            c->lane_reqs = uint32_t(v);
+    }
+    if (const char* e = std::getenv("WSG_TABLES_IN_PLACE"))
+        c->tables_in_place = *e != '0';
+    if (const char* e = std::getenv("WSG_LANE_WGS")) {
+        const long v = std::atol(e);
+        if (v >= 1 && v <= long(wsg::LANE_WGS_MAX))
+            c->lane_wgs = uint32_t(v);
+    }
     if (const char* e = std::getenv("WSG_LANE_IDLE_US")) {
         const long v = std::atol(e);
         if (v > 0 && v <= 1000000)
@@ -1168,15 +1227,33 @@ int decode_host_direct(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const
     wsg_ctx::Slot& sl = c->slots[0];
     if (int rc = slot_reserve(sl, 0, n, false))
         return rc;
-    std::memcpy(sl.h_fs, frame_start, size_t(n) * sizeof(uint64_t));
-    if (wire_len <= std::min<uint64_t>(c->lane_max, wsg::LANE_STAGE) && n > 0 && strictly_increasing(frame_start, n)) {
-        // a few KiB (an echo's read): the resident lane, no launch
-        const uint64_t a[6] = {reinterpret_cast<uint64_t>(wire), wire_len, reinterpret_cast<uint64_t>(sl.h_fs),
-                               reinterpret_cast<uint64_t>(out), reinterpret_cast<uint64_t>(sl.h_info), 0};
+    // a table and records in wsg_host_alloc blocks (the batch classes') are
+    // used where they are; others through the slot's page-locked copies
+    const uint64_t* fs_dev = frame_start;
+    if (!c->tables_in_place || !in_host_block(frame_start, uint64_t(n) * sizeof(uint64_t))) {
+        std::memcpy(sl.h_fs, frame_start, size_t(n) * sizeof(uint64_t));
+        fs_dev = sl.h_fs;
+    }
+    wsg_recv_info* info_dev =
+        c->tables_in_place && in_host_block(info, uint64_t(n) * sizeof(wsg_recv_info)) ? info : sl.h_info;
+    wsg::LaneBell* lb = nullptr;
+    if (wire_len <= std::min<uint64_t>(c->lane_max, wsg::LANE_STAGE - 64) && n > 0 && n <= lane_max_frames(c) &&
+        strictly_increasing(frame_start, n) && (lb = lane_ready(c))) {
+        // a few KiB (an echo's read): the resident lane, no launch; group
+        // k's wire range from its first start (0 for the first) to the next
+        // group's (wire_len after the last)
+        const uint32_t G = lane_group_size(c, n);
+        for (uint32_t k = 0, f = 0; f < n; ++k, f += G) {
+            lb->grp[k][0].v = k == 0 ? 0 : std::min(frame_start[f], wire_len);
+            lb->grp[k][1].v = f + G < n ? std::min(frame_start[f + G], wire_len) : wire_len;
+        }
+        const uint64_t a[6] = {reinterpret_cast<uint64_t>(wire), wire_len, reinterpret_cast<uint64_t>(fs_dev),
+                               reinterpret_cast<uint64_t>(out), reinterpret_cast<uint64_t>(info_dev), 0};
         const auto t_ring = std::chrono::steady_clock::now();
-        if (lane_call(c, wsg::LANE_DECODE, n, a) == WSG_OK) {
+        if (lane_call(c, wsg::LANE_DECODE, n, G, a) == WSG_OK) {
             const auto t_back = std::chrono::steady_clock::now();
-            std::memcpy(info, sl.h_info, size_t(n) * sizeof(wsg_recv_info));
+            if (info_dev != info)
+                std::memcpy(info, info_dev, size_t(n) * sizeof(wsg_recv_info));
             const int rc = host_batch_status(c, wire, wire_len, frame_start, n, info);
             if (c->lane_profile) {
                 using us = std::chrono::duration<double, std::micro>;
@@ -1189,10 +1266,11 @@ int decode_host_direct(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const
         // the lane did not answer: the launch path below (from now on always)
     }
     hipStream_t s = c->stream;
-    if (int rc = decode_launch(c, wire, wire_len, sl.h_fs, n, out, sl.h_info, s, c->d_err_host))
+    if (int rc = decode_launch(c, wire, wire_len, fs_dev, n, out, info_dev, s, c->d_err_host))
         return rc;
     WSG_HIP(hipStreamSynchronize(s));
-    std::memcpy(info, sl.h_info, size_t(n) * sizeof(wsg_recv_info));
+    if (info_dev != info)
+        std::memcpy(info, info_dev, size_t(n) * sizeof(wsg_recv_info));
     return host_batch_status(c, wire, wire_len, frame_start, n, info);
 }
 
@@ -1365,7 +1443,8 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
             const wsg_send_desc& d = desc[i];
             if (d.len > payload_len || d.src_off > payload_len - d.len)
                 return WSG_EINVAL;
-            wire_off[i + 1] = wire_off[i] + wsg_frame_size(d.opcode, d.mask, d.len, d.status);
+            const wsg::SendGeom g = wsg::send_geom(d.opcode, d.mask != 0, d.len, d.status);   // = wsg_frame_size
+            wire_off[i + 1] = wire_off[i] + g.hdr + g.body;
         }
         if (wire_off[n] > wire_cap)
             return WSG_ENOMEM;
@@ -1383,17 +1462,40 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
             wsg_ctx::Slot& sl = c->slots[0];
             if (int rc = slot_reserve_enc(sl, 0, wire_off[n], n, false))
                 return rc;
-            std::memcpy(sl.h_desc, desc, size_t(n) * sizeof(wsg_send_desc));
-            if (wire_off[n] <= c->lane_max) {
+            // descriptors and offsets in wsg_host_alloc blocks (the batch
+            // classes') are read where they are; others through copies
+            const wsg_send_desc* desc_dev = desc;
+            if (!c->tables_in_place || !in_host_block(desc, uint64_t(n) * sizeof(wsg_send_desc))) {
+                std::memcpy(sl.h_desc, desc, size_t(n) * sizeof(wsg_send_desc));
+                desc_dev = sl.h_desc;
+            }
+            wsg::LaneBell* lb = nullptr;
+            if (wire_off[n] <= c->lane_max && n <= lane_max_frames(c) && (lb = lane_ready(c))) {
                 // a few KiB (the replies of an echo's read): the resident
-                // lane at the offsets computed above, no launch
-                if (int rc = slot_reserve(sl, 0, uint64_t(n) + 1, false))
-                    return rc;
-                std::memcpy(sl.h_fs, wire_off, (size_t(n) + 1) * sizeof(uint64_t));
-                const uint64_t a[6] = {reinterpret_cast<uint64_t>(payload), reinterpret_cast<uint64_t>(sl.h_desc),
-                                       reinterpret_cast<uint64_t>(sl.h_fs), reinterpret_cast<uint64_t>(wire), 0, 0};
+                // lane at the offsets computed above, no launch; group k's
+                // payload span for its staging
+                const uint64_t* off_dev = wire_off;
+                if (!c->tables_in_place || !in_host_block(wire_off, (uint64_t(n) + 1) * sizeof(uint64_t))) {
+                    if (int rc = slot_reserve(sl, 0, uint64_t(n) + 1, false))
+                        return rc;
+                    std::memcpy(sl.h_fs, wire_off, (size_t(n) + 1) * sizeof(uint64_t));
+                    off_dev = sl.h_fs;
+                }
+                const uint32_t G = lane_group_size(c, n);
+                for (uint32_t k = 0, f = 0; f < n; ++k, f += G) {
+                    uint64_t lo = UINT64_MAX, hi = 0;
+                    for (uint32_t i = f, e = std::min(n, f + G); i < e; ++i)
+                        if (desc[i].len) {
+                            lo = std::min(lo, desc[i].src_off);
+                            hi = std::max(hi, desc[i].src_off + desc[i].len);
+                        }
+                    lb->grp[k][0].v = hi ? lo : 0;
+                    lb->grp[k][1].v = hi;
+                }
+                const uint64_t a[6] = {reinterpret_cast<uint64_t>(payload), reinterpret_cast<uint64_t>(desc_dev),
+                                       reinterpret_cast<uint64_t>(off_dev), reinterpret_cast<uint64_t>(wire), 0, 0};
                 const auto t_ring = std::chrono::steady_clock::now();
-                if (lane_call(c, wsg::LANE_ENCODE, n, a) == WSG_OK) {
+                if (lane_call(c, wsg::LANE_ENCODE, n, G, a) == WSG_OK) {
                     if (c->lane_profile) {
                         c->lane_prof[0] += std::chrono::duration<double, std::micro>(t_ring - t_in).count();
                         ++c->lane_prof_n;
@@ -1402,7 +1504,7 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
                 }
             }
             hipStream_t s = c->stream;
-            if (int rc = encode_launch(c, s, payload, sl.h_desc, n, wire, wire_off[n], sl.d_woff, sl.enc,
+            if (int rc = encode_launch(c, s, payload, desc_dev, n, wire, wire_off[n], sl.d_woff, sl.enc,
                                        c->d_err_host))
                 return rc;
             WSG_HIP(hipStreamSynchronize(s));

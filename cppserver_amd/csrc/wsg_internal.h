@@ -108,24 +108,47 @@ hipError_t launch_test_spin(hipStream_t s, uint32_t us);
 enum : uint32_t { LANE_DECODE = 1, LANE_ENCODE = 2 };
 constexpr uint32_t LANE_THREADS = 1024;   // one workgroup; frames per group (lane per frame)
 constexpr uint64_t LANE_STAGE = 64 << 10;  // decode: wire bytes staged in LDS (the lane's batch limit)
-// LDS of the lane: decode's staged wire + info blocks + payload bounds and
-// keys; encode's offsets, heads, records and staged descriptors fit inside
-constexpr uint64_t LANE_LDS = LANE_STAGE + 32 * LANE_THREADS + 20 * LANE_THREADS;
-struct LaneBell {
-    uint64_t seq;       // host: request number (written last, release)
-    uint32_t op, n;     // host: LANE_* and frame count
-    uint64_t a[6];      // host: arguments (device-visible host addresses, sizes)
-    uint64_t pad0[8];
-    uint64_t done;      // lane: last request answered (release)
-    uint64_t pad1[7];
-    uint32_t stop;      // host: leave now
-    uint32_t exited;    // lane: has left (its last store)
-    uint64_t pad2[7];
+constexpr uint64_t LANE_PSTAGE = 64 << 10; // encode: payload arena staged in LDS when its 16-B blocks fit
+// LDS of the lane (one layout per op, the larger sized):
+//   decode: staged wire | info blocks (32 B) | payload bounds (2 x 8 B), key (4 B), frame starts (8 B) per frame
+//   encode: offsets (8 B) | heads (16 B) | records (16 B) | descriptors (32 B) per frame | staged payload
+constexpr uint64_t LANE_LDS_DECODE = LANE_STAGE + 60 * LANE_THREADS + 64;
+constexpr uint64_t LANE_LDS_ENCODE = 72 * LANE_THREADS + 64 + LANE_PSTAGE;
+constexpr uint64_t LANE_LDS = LANE_LDS_DECODE > LANE_LDS_ENCODE ? LANE_LDS_DECODE : LANE_LDS_ENCODE;
+static_assert(LANE_LDS <= 160 * 1024 - 1024, "the lane's workgroup LDS");
+constexpr uint32_t LANE_WGS_MAX = 16;          // workgroups of the lane (each a CU's worth of LDS)
+constexpr uint32_t LANE_GROUPS_MAX = 32;       // frame groups of a request (<= 32 Ki frames)
+constexpr uint32_t LANE_GROUPS_PER_WG = 4;     // groups one workgroup takes (LANE_GROUPS_MAX / 8 workgroups)
+constexpr uint32_t LANE_WORDS = 8;             // request words (w[])
+// A request word and the number of the request it belongs to (the host
+// stores v, then tag; the lane reads the 16 bytes in one request).
+struct alignas(16) LaneUnit {
+    uint64_t v, tag;
 };
+struct LaneBell {
+    LaneUnit w[LANE_WORDS];                // host: op | n << 32, a[0..5], G | profile << 32
+    LaneUnit grp[LANE_GROUPS_MAX][2];      // host: group k's range (decode: wire [lo, hi); encode: payload span)
+    uint64_t done[LANE_WGS_MAX];           // lane: workgroup g's last request answered (its tag, release)
+    uint64_t prof[8];                      // lane: workgroup 0's phase clocks ($WSG_LANE_PROFILE)
+    uint32_t stop;                         // host: leave now
+    uint32_t pad1[15];
+    uint32_t exited[LANE_WGS_MAX];         // lane: workgroup g of launch `gen` has left (its last store)
+};
+// Request: G frames per group (1..LANE_THREADS), groups k = 0.. of frames
+// [k G, min(n, (k + 1) G)); workgroup g takes groups g, g + nw, ... (at most
+// LANE_GROUPS_PER_WG: the host picks G so).
 // decode: a = {wire, wire_len, frame_start, out, info}; the table strictly
-//         increasing (the caller checks) — bit-identical to k_decode there
-// encode: a = {payload, desc, wire_off (n + 1, host-computed), wire}
-hipError_t launch_lane(hipStream_t s, LaneBell* bell, uint64_t idle_ticks);
+//         increasing (the caller checks), wire_len + 64 <= LANE_STAGE;
+//         grp[k] = {lo, hi}: k's first start (0 for k = 0) and the next
+//         group's (wire_len for the last), both clamped to wire_len —
+//         bit-identical to k_decode there
+// encode: a = {payload, desc, wire_off (n + 1, host-computed), wire};
+//         grp[k] = the payload span [lo, hi) of k's frames ({0, 0}: none)
+// A launch ends after idle_ticks without a request, on `stop`, or after
+// answering a request whose number is a multiple of `reqs` (gen: the
+// launch's number, >= 1, what its workgroups store in exited[]).
+hipError_t launch_lane(hipStream_t s, LaneBell* bell, uint32_t workgroups, uint64_t idle_ticks, uint32_t gen,
+                       uint32_t reqs);
 
 // HIP device a context is bound to (wsg_capi.hip)
 int ctx_device(const wsg_ctx* c);

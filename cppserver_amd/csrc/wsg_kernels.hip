@@ -99,6 +99,14 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #define WSG_NT_STORE 1
 #endif
 __device__ __forceinline__ v4u ld16(const uint8_t* p) { return *reinterpret_cast<const v4u*>(p); }
+// 16 bytes of host memory in one request past the GPU's caches (the system
+// scope of the relaxed atomic loads, sc0 sc1): one snapshot of the 16 bytes.
+__device__ __forceinline__ v4u ld16_sys(const void* p)
+{
+    v4u r;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+    return r;
+}
 __device__ __forceinline__ v4u ld16nt(const uint8_t* p)
 {
     if (WSG_NT_LOAD)
@@ -906,7 +914,20 @@ __device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirs
 // 16 payload bytes as seen from a chunk: byte j = payload[c + j] where that
 // offset is inside [0, len) (else 0).  Reads only aligned 16-B blocks that
 // hold a wanted byte, at most two.
-__device__ __forceinline__ v4u fan_window(const uint8_t* __restrict__ payload, uint64_t len, int64_t c)
+// The 16-B block at an aligned address: a global load, or (the lane) the
+// block's copy staged in LDS.
+struct GlobalBlocks {
+    __device__ v4u operator()(const uint8_t* p) const { return ld16(p); }
+};
+struct StagedBlocks {
+    const v4u* s;          // LDS copy of the aligned blocks from `base` on
+    const uint8_t* base;   // 16-B aligned
+    __device__ v4u operator()(const uint8_t* p) const { return s[(p - base) >> 4]; }
+};
+
+template <class Blocks = GlobalBlocks>
+__device__ __forceinline__ v4u fan_window(const uint8_t* __restrict__ payload, uint64_t len, int64_t c,
+                                          Blocks blk = Blocks{})
 {
     // offsets relative to `payload`, loads through pointer arithmetic on it
     // (global_* loads; a pointer rebuilt from an integer loads flat_*)
@@ -915,9 +936,9 @@ __device__ __forceinline__ v4u fan_window(const uint8_t* __restrict__ payload, u
     const int64_t n = int64_t(len);
     v4u lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
     if (r0 < n && r0 + 16 > 0)
-        lo = ld16(payload + r0);
+        lo = blk(payload + r0);
     if (s != 0 && r0 + 16 < n && r0 + 32 > 0)
-        hi = ld16(payload + r0 + 16);
+        hi = blk(payload + r0 + 16);
     return s ? funnel(lo, hi, s) : lo;
 }
 
@@ -1406,15 +1427,16 @@ struct SmallFrame {
 };
 
 // Bytes [o, o + 16) of a frame of fsize bytes (o < fsize), 0 past its end.
+template <class Blocks = GlobalBlocks>
 __device__ __forceinline__ v4u small_bytes(const uint8_t* __restrict__ payload, v4u head, const SmallFrame& f,
-                                          uint64_t fsize, uint64_t o)
+                                          uint64_t fsize, uint64_t o, Blocks blk = Blocks{})
 {
     const uint32_t data0 = f.geo & 0xFFu, hdr = f.geo >> 8;
     v4u out = shr_bytes(head, o);
     const uint64_t lo = o < data0 ? data0 - o : 0;   // chunk bytes [lo, hi) are payload
     const uint64_t hi = fsize - o < CHUNK ? fsize - o : CHUNK;
     if (lo < hi) {
-        const v4u w = fan_window(payload + f.src, fsize - data0, int64_t(o) - int64_t(data0));
+        const v4u w = fan_window(payload + f.src, fsize - data0, int64_t(o) - int64_t(data0), blk);
         out |= (w ^ key_rot(f.key, uint32_t(o - hdr))) & (low_bytes(hi) & ~low_bytes(lo));
     }
     return out;
@@ -1441,9 +1463,11 @@ __device__ __forceinline__ uint64_t small_head(const Desc& d, v4u& h, SmallFrame
 // 0..cnt-1 of the group, LDS: offsets, heads, records), lanes t, t + nt, ...:
 // each chunk ORs together the frames it overlaps; only the range's first and
 // last chunk, shared with the neighbouring groups, get byte stores.
+template <class Blocks = GlobalBlocks>
 __device__ __forceinline__ void small_chunks(const uint8_t* __restrict__ payload, const uint64_t* s_off,
                                              const v4u* s_head, const SmallFrame* s_fr, uint32_t cnt,
-                                             uint8_t* __restrict__ wire, uint32_t t, uint32_t nt)
+                                             uint8_t* __restrict__ wire, uint32_t t, uint32_t nt,
+                                             Blocks blk = Blocks{})
 {
     const uint64_t r_lo = s_off[0], r_hi = s_off[cnt];
     for (uint64_t p = (r_lo & ~uint64_t(CHUNK - 1)) + uint64_t(t) * CHUNK; p < r_hi; p += uint64_t(nt) * CHUNK) {
@@ -1462,9 +1486,9 @@ __device__ __forceinline__ void small_chunks(const uint8_t* __restrict__ payload
                 break;
             const uint64_t fsize = s_off[j + 1] - off;
             if (p >= off)
-                w |= small_bytes(payload, s_head[j], s_fr[j], fsize, p - off);
+                w |= small_bytes(payload, s_head[j], s_fr[j], fsize, p - off, blk);
             else
-                w |= shl_bytes(small_bytes(payload, s_head[j], s_fr[j], fsize, 0), off - p);
+                w |= shl_bytes(small_bytes(payload, s_head[j], s_fr[j], fsize, 0, blk), off - p);
         }
         if (p >= r_lo && p + CHUNK <= r_hi) {
             st16nt(wire + p, w);
@@ -1554,222 +1578,330 @@ __global__ __launch_bounds__(BLOCK) void k_encode_small(const uint8_t* __restric
 // ---- the host lane (wsg_internal.h) ----------------------------------------
 
 // The lane reads its host inputs in whole, coalesced 16-byte blocks into
-// LDS first: one workgroup has few memory requests in flight, and every
-// round trip over PCIe costs microseconds (a lane-per-frame read of 32-byte
-// descriptors or headers scattered over lines took several).
-__device__ __forceinline__ void lane_stage(v4u* dst, const uint8_t* __restrict__ src, uint64_t blocks)
-{
-    for (uint64_t c = threadIdx.x; c < blocks; c += LANE_THREADS)
-        dst[c] = ld16(src + c * CHUNK);
-}
+// LDS, every load of a step issued before any is waited for: one workgroup
+// has few requests in flight, and each PCIe round trip costs microseconds
+// (a lane-per-frame read of 32-byte descriptors or headers scattered over
+// lines took several; one block per lane per round trip, three for an
+// echo's read, $WSG_LANE_PROFILE).  `U` blocks per lane at most.
+template <int U>
+struct LaneLoads {
+    v4u v[U];
+    __device__ __forceinline__ void load(const uint8_t* __restrict__ src, uint64_t blocks, bool on)
+    {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = threadIdx.x + uint64_t(u) * LANE_THREADS;
+            if (on && k < blocks)
+                v[u] = ld16(src + k * CHUNK);
+        }
+    }
+    __device__ __forceinline__ void store(v4u* dst, uint64_t blocks, bool on) const
+    {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = threadIdx.x + uint64_t(u) * LANE_THREADS;
+            if (on && k < blocks)
+                dst[k] = v[u];
+        }
+    }
+};
 
-// Encode of a host batch on the lane: groups of LANE_THREADS frames; the
-// group's descriptors staged, one lane per frame builds its head
-// (small_head), then the group's chunks (small_chunks): the bytes
-// k_encode_small writes, at the host's offsets.
-__device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload, const wsg_send_desc* __restrict__ desc,
-                                            uint32_t n, const uint64_t* __restrict__ wire_off,
-                                            uint8_t* __restrict__ wire, uint8_t* lds, uint64_t* ts)
+// Encode of one frame group on the lane (frames [f_lo, f_lo + cnt)): its
+// offsets and descriptors — and its frames' payload span [plo, phi) when that
+// span's 16-B blocks fit LANE_PSTAGE — staged in one round trip, a lane per
+// frame builds its head (small_head), then the group's chunks (small_chunks,
+// payload windows from LDS): the bytes k_encode_small writes, at the host's
+// offsets.  The range's first and last chunk, shared with the neighbouring
+// groups (other workgroups), get byte stores.
+__device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload, uint64_t plo, uint64_t phi,
+                                            const wsg_send_desc* __restrict__ desc, uint32_t f_lo, uint32_t cnt,
+                                            const uint64_t* __restrict__ wire_off, uint8_t* __restrict__ wire,
+                                            uint8_t* lds, uint64_t* ts)
 {
     uint64_t* s_off = reinterpret_cast<uint64_t*>(lds);                             // LANE_THREADS + 1 (+1 pad)
     v4u* s_head = reinterpret_cast<v4u*>(lds + 8 * (LANE_THREADS + 2));
     SmallFrame* s_fr = reinterpret_cast<SmallFrame*>(s_head + LANE_THREADS);
     v4u* s_desc = reinterpret_cast<v4u*>(s_fr + LANE_THREADS);                       // 2 blocks per descriptor
+    v4u* s_pay = s_desc + 2 * LANE_THREADS;                                          // LANE_PSTAGE
     static_assert(sizeof(wsg_send_desc) == 32 && sizeof(SmallFrame) == 16, "lane LDS layout");
+    static_assert(8 * (LANE_THREADS + 2) + 64 * LANE_THREADS + LANE_PSTAGE <= LANE_LDS, "lane LDS layout");
     const uint32_t t = threadIdx.x;
-    for (uint32_t f_lo = 0; f_lo < n; f_lo += LANE_THREADS) {
-        const uint32_t cnt = min(n - f_lo, LANE_THREADS);
-        lane_stage(s_desc, reinterpret_cast<const uint8_t*>(desc + f_lo), 2 * uint64_t(cnt));
-        if (t < cnt) {
-            s_off[t] = wire_off[f_lo + t];
-            if (t + 1 == cnt)
-                s_off[cnt] = wire_off[f_lo + cnt];
-        }
-        __syncthreads();
-        ts[0] = wall_clock64();
-        if (t < cnt) {
-            const Desc d = load_desc(reinterpret_cast<const wsg_send_desc*>(s_desc) + t);
-            (void)small_head(d, s_head[t], s_fr[t]);
-        }
-        __syncthreads();
-        ts[1] = wall_clock64();
-        if (WSG_LANE_DIAG != 2)   // (DIAG 2, timing only: the per-frame phase alone)
+    // the span's aligned blocks (payload + plo rounded down)
+    const uint8_t* p0 = payload + plo;
+    p0 -= reinterpret_cast<uintptr_t>(p0) & (CHUNK - 1);
+    const uint64_t pblocks = phi > plo ? (uint64_t(payload + phi - p0) + CHUNK - 1) / CHUNK : 0;
+    const bool staged = pblocks <= LANE_PSTAGE / CHUNK;
+    uint64_t off = 0, off_end = 0;
+    if (t < cnt)
+        off = wire_off[f_lo + t];
+    if (t + 1 == cnt)
+        off_end = wire_off[f_lo + cnt];
+    LaneLoads<2> dl;
+    dl.load(reinterpret_cast<const uint8_t*>(desc + f_lo), 2 * uint64_t(cnt), true);
+    LaneLoads<LANE_PSTAGE / CHUNK / LANE_THREADS> pl;
+    pl.load(p0, pblocks, staged);
+    if (t < cnt)
+        s_off[t] = off;
+    if (t + 1 == cnt)
+        s_off[cnt] = off_end;
+    dl.store(s_desc, 2 * uint64_t(cnt), true);
+    pl.store(s_pay, pblocks, staged);
+    __syncthreads();
+    ts[0] = wall_clock64();
+    if (t < cnt) {
+        const Desc d = load_desc(reinterpret_cast<const wsg_send_desc*>(s_desc) + t);
+        (void)small_head(d, s_head[t], s_fr[t]);
+    }
+    __syncthreads();
+    ts[1] = wall_clock64();
+    if (WSG_LANE_DIAG != 2) {   // (DIAG 2, timing only: the per-frame phase alone)
+        if (staged)
+            small_chunks(payload, s_off, s_head, s_fr, cnt, wire, t, LANE_THREADS, StagedBlocks{s_pay, p0});
+        else
             small_chunks(payload, s_off, s_head, s_fr, cnt, wire, t, LANE_THREADS);
-        __syncthreads();   // the group's LDS is reused by the next
     }
 }
 
-// Decode of a host batch on the lane (frame table strictly increasing, the
-// wire at most LANE_STAGE bytes): the wire staged into LDS; groups of
-// LANE_THREADS frames, a lane per frame parses it (frame_parse_b: k_decode's
-// rules) into LDS, the group's wsg_recv_info go out in whole blocks; then the
-// group's wire range — from its first frame's start (0 for the first group)
-// to the next group's (wire_len for the last) — chunk by chunk: the wire
-// bytes, the valid frames' payload bytes XORed with their keys.  Out-of-range
-// and error frames' bytes are copied, as k_decode does.
-__device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, uint64_t wire_len,
-                                            const uint64_t* __restrict__ fs, uint32_t n, uint8_t* out,
-                                            wsg_recv_info* __restrict__ info, uint8_t* lds, uint64_t* ts)
+// Decode of one frame group on the lane (frame table strictly increasing,
+// the wire at most LANE_STAGE - 64 bytes): the group's frame starts and its
+// wire range [lo, hi) — from its first frame's start (0 for the first group)
+// to the next group's (wire_len for the last) — plus the 32 bytes a header
+// read may look past hi, staged in one round trip; a lane per frame parses
+// it (frame_parse_b: k_decode's rules) into LDS, the group's wsg_recv_info go
+// out in whole blocks; then the range chunk by chunk: the wire bytes, the
+// valid frames' payload bytes XORed with their keys.  Out-of-range and error
+// frames' bytes are copied, as k_decode does.  (In place, a header that runs
+// past hi — a table breaking the no-overlap contract — may read bytes the
+// next group's workgroup has already unmasked, as k_decode's blocks may.)
+__device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, uint64_t wire_len, uint64_t lo,
+                                            uint64_t hi, const uint64_t* __restrict__ fs, uint32_t n, uint32_t f_lo,
+                                            uint32_t cnt, uint8_t* out, wsg_recv_info* __restrict__ info,
+                                            uint8_t* lds, uint64_t* ts)
 {
     v4u* s_wire = reinterpret_cast<v4u*>(lds);
     v4u* s_info = reinterpret_cast<v4u*>(lds + LANE_STAGE);                          // 2 blocks per record
     uint64_t* s_pl = reinterpret_cast<uint64_t*>(s_info + 2 * LANE_THREADS);
     uint64_t* s_pe = s_pl + LANE_THREADS;
     uint32_t* s_key = reinterpret_cast<uint32_t*>(s_pe + LANE_THREADS);
+    uint64_t* s_fs = reinterpret_cast<uint64_t*>(s_key + LANE_THREADS);               // the group's starts + next
     static_assert(sizeof(wsg_recv_info) == 32, "lane LDS layout");
+    static_assert(LANE_STAGE + 60 * LANE_THREADS + 8 <= LANE_LDS, "lane LDS layout");
     const uint32_t t = threadIdx.x;
-    lane_stage(s_wire, wire, (wire_len + CHUNK - 1) / CHUNK);
+    const uint64_t sb = lo & ~uint64_t(CHUNK - 1);
+    const uint64_t se = min(hi + 32, wire_len);
+    const uint64_t wblocks = se > sb ? (se - sb + CHUNK - 1) / CHUNK : 0;   // <= LANE_STAGE / CHUNK (host)
+    const auto block = [s_wire, sb](uint64_t a) { return s_wire[(a - sb) / CHUNK]; };
+    uint64_t st = 0, nx = wire_len;
+    if (t < cnt)
+        st = fs[f_lo + t];
+    if (t + 1 == cnt && f_lo + cnt < n)
+        nx = fs[f_lo + cnt];
+    LaneLoads<LANE_STAGE / CHUNK / LANE_THREADS> wl;
+    wl.load(wire + sb, wblocks, true);
+    if (t < cnt)
+        s_fs[t] = st;
+    if (t + 1 == cnt)
+        s_fs[cnt] = nx;
+    wl.store(s_wire, wblocks, true);
     __syncthreads();
-    ts[0] = wall_clock64();   // (thread 0's is the one reported: $WSG_LANE_PROFILE)
-    const auto block = [s_wire](uint64_t a) { return s_wire[a / CHUNK]; };
-    for (uint32_t f_lo = 0; f_lo < n; f_lo += LANE_THREADS) {
-        const uint32_t cnt = min(n - f_lo, LANE_THREADS);
-        if (t < cnt) {
-            const uint32_t i = f_lo + t;
-            const uint64_t st = fs[i];
-            const uint64_t limit = i + 1 < n ? fs[i + 1] : wire_len;
-            wsg_recv_info r;
-            const int e = frame_parse_b(block, wire_len, st, limit, r);
-            store_info(reinterpret_cast<wsg_recv_info*>(s_info) + t, r);
-            const uint64_t pl = e ? st : r.payload_off;
-            s_pl[t] = pl;
-            s_pe[t] = e ? st : pl + r.len;
-            s_key[t] = (e == 0 && r.masked) ? r.key : 0u;
+    ts[0] = wall_clock64();   // (thread 0's of workgroup 0 is the one reported: $WSG_LANE_PROFILE)
+    if (t < cnt) {
+        const uint64_t st = s_fs[t];
+        const uint64_t limit = s_fs[t + 1];   // the next frame's start, wire_len after the last
+        wsg_recv_info r;
+        const int e = frame_parse_b(block, wire_len, st, limit, r);
+        store_info(reinterpret_cast<wsg_recv_info*>(s_info) + t, r);
+        const uint64_t pl = e ? st : r.payload_off;
+        s_pl[t] = pl;
+        s_pe[t] = e ? st : pl + r.len;
+        s_key[t] = (e == 0 && r.masked) ? r.key : 0u;
+    }
+    __syncthreads();
+    ts[1] = wall_clock64();
+    {
+        v4u* dst = reinterpret_cast<v4u*>(info + f_lo);
+        for (uint32_t k = t; k < 2 * cnt; k += LANE_THREADS)
+            dst[k] = s_info[k];
+    }
+    if (WSG_LANE_DIAG == 2)   // timing only: the per-frame phase alone
+        return;
+    for (uint64_t p = sb + uint64_t(t) * CHUNK; p < hi; p += uint64_t(LANE_THREADS) * CHUNK) {
+        const v4u wv = s_wire[(p - sb) / CHUNK];
+        // last frame whose payload starts at or before p (frame 0 if none)
+        uint32_t a = 0, b = cnt - 1;
+        while (a < b) {
+            const uint32_t m = (a + b + 1) >> 1;
+            if (s_pl[m] <= p)
+                a = m;
+            else
+                b = m - 1;
         }
-        __syncthreads();
-        ts[1] = wall_clock64();
-        {
-            v4u* dst = reinterpret_cast<v4u*>(info + f_lo);
-            for (uint32_t k = t; k < 2 * cnt; k += LANE_THREADS)
-                dst[k] = s_info[k];
-        }
-        const uint64_t lo = min(f_lo == 0 ? uint64_t(0) : fs[f_lo], wire_len);
-        const uint64_t hi = min(f_lo + cnt < n ? fs[f_lo + cnt] : wire_len, wire_len);
-        if (WSG_LANE_DIAG == 2) {   // timing only: the per-frame phase alone
-            __syncthreads();
-            continue;
-        }
-        for (uint64_t p = (lo & ~uint64_t(CHUNK - 1)) + uint64_t(t) * CHUNK; p < hi; p += uint64_t(LANE_THREADS) * CHUNK) {
-            const v4u wv = s_wire[p / CHUNK];
-            // last frame whose payload starts at or before p (frame 0 if none)
-            uint32_t a = 0, b = cnt - 1;
-            while (a < b) {
-                const uint32_t m = (a + b + 1) >> 1;
-                if (s_pl[m] <= p)
-                    a = m;
-                else
-                    b = m - 1;
-            }
-            v4u m = {0, 0, 0, 0};
-            for (uint32_t j = a; j < cnt; ++j) {
-                const uint64_t pl = s_pl[j], pe = s_pe[j];
-                if (pl >= p + CHUNK)
-                    break;
-                const uint32_t key = s_key[j];
-                if (key == 0 || pe <= p)
-                    continue;
-                if (pl <= p && pe >= p + CHUNK) {   // the chunk lies in this payload
-                    const uint32_t kw = key_rot(key, uint32_t(p - pl));
-                    m ^= v4u{kw, kw, kw, kw};
-                } else {   // the payload's bytes of the chunk: [max(pl, p), min(pe, p + 16))
-                    const uint32_t kw = key_rot(key, uint32_t(p - pl));   // (mod 4 also when p < pl)
-                    const uint64_t b0 = pl > p ? pl - p : 0, b1 = pe - p < CHUNK ? pe - p : CHUNK;
-                    m ^= v4u{kw, kw, kw, kw} & (low_bytes(b1) & ~low_bytes(b0));
-                }
-            }
-            const v4u w = wv ^ m;
-            if (p >= lo && p + CHUNK <= hi) {
-                st16nt(out + p, w);
-            } else {
-                const uint32_t j0 = p < lo ? uint32_t(lo - p) : 0;
-                const uint32_t j1 = hi - p < CHUNK ? uint32_t(hi - p) : CHUNK;
-                for (uint32_t j = j0; j < j1; ++j)
-                    out[p + j] = uint8_t(lane_byte(w, j));
+        v4u m = {0, 0, 0, 0};
+        for (uint32_t j = a; j < cnt; ++j) {
+            const uint64_t pl = s_pl[j], pe = s_pe[j];
+            if (pl >= p + CHUNK)
+                break;
+            const uint32_t key = s_key[j];
+            if (key == 0 || pe <= p)
+                continue;
+            if (pl <= p && pe >= p + CHUNK) {   // the chunk lies in this payload
+                const uint32_t kw = key_rot(key, uint32_t(p - pl));
+                m ^= v4u{kw, kw, kw, kw};
+            } else {   // the payload's bytes of the chunk: [max(pl, p), min(pe, p + 16))
+                const uint32_t kw = key_rot(key, uint32_t(p - pl));   // (mod 4 also when p < pl)
+                const uint64_t b0 = pl > p ? pl - p : 0, b1 = pe - p < CHUNK ? pe - p : CHUNK;
+                m ^= v4u{kw, kw, kw, kw} & (low_bytes(b1) & ~low_bytes(b0));
             }
         }
-        __syncthreads();
+        const v4u w = wv ^ m;
+        if (p >= lo && p + CHUNK <= hi) {
+            st16nt(out + p, w);
+        } else {
+            const uint32_t j0 = p < lo ? uint32_t(lo - p) : 0;
+            const uint32_t j1 = hi - p < CHUNK ? uint32_t(hi - p) : CHUNK;
+            for (uint32_t j = j0; j < j1; ++j)
+                out[p + j] = uint8_t(lane_byte(w, j));
+        }
     }
 }
 
-__global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ bell, uint64_t idle_ticks)
+// The lane: gridDim.x workgroups, each polling the doorbell and taking the
+// frame groups g, g + nw, ... of every request (groups of `G` frames, the
+// host's per-group ranges in bell->grp), answering in its own done word.
+// The workgroups never wait on each other: each stages, works and answers
+// alone, so the request's PCIe reads and writes spread over nw CUs (one CU
+// has few requests in flight: one workgroup took ~5 us to stage a 38 KB
+// read and ~7 us to write it back, $WSG_LANE_PROFILE).
+__global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ bell, uint64_t idle_ticks, uint32_t gen,
+                                                       uint32_t reqs)
 {
-    __shared__ uint64_t s_a[6];
-    __shared__ uint32_t s_op, s_n;
+    __shared__ uint64_t s_tag;
+    __shared__ uint64_t s_w[LANE_WORDS];
+    __shared__ uint64_t s_g[LANE_GROUPS_PER_WG][2];
     __shared__ int s_go;
     __shared__ v4u s_mem[LANE_LDS / 16];   // the op's staging (lane_decode / lane_encode layouts)
-    const uint32_t t = threadIdx.x;
+    const uint32_t t = threadIdx.x, g = blockIdx.x, nw = gridDim.x;
     uint64_t last = 0, seq = 0, t_seen = 0;
     uint64_t ts[2] = {0, 0};
-    if (t == 0)
-        last = __hip_atomic_load(&bell->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the units this workgroup polls: lanes 0..7 the request words, 8..15
+    // the ranges of its groups g + j nw (j < LANE_GROUPS_PER_WG)
+    const LaneUnit* unit = nullptr;
+    if (t < LANE_WORDS) {
+        unit = &bell->w[t];
+    } else if (t < LANE_WORDS + 2 * LANE_GROUPS_PER_WG) {
+        const uint32_t j = (t - LANE_WORDS) >> 1, k = g + j * nw;
+        if (k < LANE_GROUPS_MAX)
+            unit = &bell->grp[k][(t - LANE_WORDS) & 1];
+    }
+    if (t < 64)
+        last = uni(__hip_atomic_load(&bell->done[g], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
     for (;;) {
-        if (t == 0) {
+        if (t < 64) {
+            // lane 0 of wave 0 polls the request's first word, which the
+            // host stores last (each unit: its value, then its tag; x86
+            // stores are seen in program order), so a new tag there means
+            // every unit of the request is written; then lanes 0..15 read
+            // the units this workgroup needs in one round trip.  (Polling
+            // all 16 units every time saved that round trip, ~2 us, but the
+            // lanes of four threads' contexts then kept PCIe busy with
+            // their polls: 100 echo clients on 4 threads 36 -> 17 M msg/s,
+            // profiles/r4/lane_poll_ab.log.)
             int go = 0;
+            uint64_t val = 0;
             const uint64_t t0 = wall_clock64();
             // at most ~2^22 polls of >= 1 us each: ends even if the clock stalls
             for (uint32_t it = 0; it < (1u << 22); ++it) {
-                // polled relaxed, acquired once below (an acquire per poll
-                // would invalidate the caches on every iteration)
-                seq = __hip_atomic_load(&bell->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (seq != last) {
-                    __atomic_thread_fence(__ATOMIC_ACQUIRE);   // (system scope: the host's request bytes)
+                const v4u u = t == 0 ? ld16_sys(unit) : v4u{0, 0, 0, 0};
+                const uint64_t T = uni(uint64_t(u.z) | (uint64_t(u.w) << 32));
+                if (T != last) {
+                    __atomic_thread_fence(__ATOMIC_ACQUIRE);   // (system scope: the request's host buffers)
+                    seq = T;
                     go = 1;
                     break;
                 }
                 // (stop and the clock every 16th poll: each PCIe read is a
                 // round trip the next request would wait behind)
-                if ((it & 15) == 15 &&
-                    (__hip_atomic_load(&bell->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                     wall_clock64() - t0 > idle_ticks))
-                    break;
+                if ((it & 15) == 15) {
+                    uint32_t quit = 0;
+                    if (t == 0)
+                        quit = __hip_atomic_load(&bell->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                               wall_clock64() - t0 > idle_ticks;
+                    if (uni(quit))
+                        break;
+                }
                 __builtin_amdgcn_s_sleep(1);
             }
-            if (go)
-                t_seen = wall_clock64();
-            s_go = go;
+            if (go) {
+                // the units, tags checked (always the new one: written
+                // before the first word's)
+                for (;;) {
+                    const v4u u = unit ? ld16_sys(unit) : v4u{0, 0, 0, 0};
+                    const uint64_t tag = uint64_t(u.z) | (uint64_t(u.w) << 32);
+                    val = uint64_t(u.x) | (uint64_t(u.y) << 32);
+                    if (__ballot(unit && tag != seq) == 0)
+                        break;
+                }
+            }
+            if (go) {
+                if (t == 0)
+                    t_seen = wall_clock64();
+                if (t < LANE_WORDS)
+                    s_w[t] = val;
+                else if (t < LANE_WORDS + 2 * LANE_GROUPS_PER_WG)
+                    s_g[(t - LANE_WORDS) >> 1][(t - LANE_WORDS) & 1] = unit ? val : 0;
+            }
+            if (t == 0) {
+                s_go = go;
+                s_tag = seq;
+            }
         }
         __syncthreads();
         if (!s_go)
             break;
-        // the request's words (op | n, a[0..5]) in one round trip: a lane
-        // each (one after another from thread 0 they were seven PCIe reads,
-        // ~10 us before any work, $WSG_LANE_PROFILE)
-        if (t < 7) {
-            const uint64_t* words = reinterpret_cast<const uint64_t*>(&bell->op);
-            __atomic_thread_fence(__ATOMIC_ACQUIRE);   // (after thread 0's sight of seq: the barrier above)
-            const uint64_t v = __hip_atomic_load(words + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (t == 0) {
-                s_op = uint32_t(v);
-                s_n = uint32_t(v >> 32);
-            } else {
-                s_a[t - 1] = v;
-            }
-        }
-        __syncthreads();
-        const uint32_t op = WSG_LANE_DIAG == 1 ? 0u : s_op, n = s_n;   // DIAG 1: answer without the work (timing only)
+        const uint32_t op = WSG_LANE_DIAG == 1 ? 0u : uint32_t(s_w[0]);   // DIAG 1: answer without the work (timing only)
+        const uint32_t n = uint32_t(s_w[0] >> 32);
+        const uint32_t G = uint32_t(s_w[7]);   // frames per group, 1..LANE_THREADS
+        const bool profile = (s_w[7] >> 32) != 0;
         uint8_t* lds = reinterpret_cast<uint8_t*>(s_mem);
-        if (op == LANE_DECODE)
-            lane_decode(reinterpret_cast<const uint8_t*>(s_a[0]), s_a[1], reinterpret_cast<const uint64_t*>(s_a[2]), n,
-                        reinterpret_cast<uint8_t*>(s_a[3]), reinterpret_cast<wsg_recv_info*>(s_a[4]), lds, ts);
-        else if (op == LANE_ENCODE)
-            lane_encode(reinterpret_cast<const uint8_t*>(s_a[0]), reinterpret_cast<const wsg_send_desc*>(s_a[1]), n,
-                        reinterpret_cast<const uint64_t*>(s_a[2]), reinterpret_cast<uint8_t*>(s_a[3]), lds, ts);
+        const uint32_t groups = G ? (n + G - 1) / G : 0;
+        for (uint32_t j = 0; op && j < LANE_GROUPS_PER_WG; ++j) {
+            const uint32_t k = g + j * nw;
+            if (k >= groups)
+                break;
+            const uint32_t f_lo = k * G, cnt = min(n - f_lo, G);
+            if (op == LANE_DECODE)
+                lane_decode(reinterpret_cast<const uint8_t*>(s_w[1]), s_w[2], s_g[j][0], s_g[j][1],
+                            reinterpret_cast<const uint64_t*>(s_w[3]), n, f_lo, cnt, reinterpret_cast<uint8_t*>(s_w[4]),
+                            reinterpret_cast<wsg_recv_info*>(s_w[5]), lds, ts);
+            else if (op == LANE_ENCODE)
+                lane_encode(reinterpret_cast<const uint8_t*>(s_w[1]), s_g[j][0], s_g[j][1],
+                            reinterpret_cast<const wsg_send_desc*>(s_w[2]), f_lo, cnt,
+                            reinterpret_cast<const uint64_t*>(s_w[3]), reinterpret_cast<uint8_t*>(s_w[4]), lds, ts);
+            __syncthreads();   // the group's LDS is reused by the next
+        }
         __syncthreads();
         if (t == 0) {
             const uint64_t t_work = wall_clock64();
             __threadfence_system();   // the request's stores are visible to the host before its answer
-            if (s_a[5]) {   // $WSG_LANE_PROFILE: the request's phases on the constant clock
+            if (profile && g == 0) {   // $WSG_LANE_PROFILE: the request's phases on the constant clock
                 const uint64_t t_fenced = wall_clock64();
                 const uint64_t v[5] = {t_seen, ts[0], ts[1], t_work, t_fenced};
                 for (int k = 0; k < 5; ++k)
-                    __hip_atomic_store(&bell->pad0[k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&bell->prof[k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
-            __hip_atomic_store(&bell->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            last = seq;
+            __hip_atomic_store(&bell->done[g], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        last = seq;   // (wave 0's lanes: the tag they saw)
+        // every `reqs`-th request the lane ends after answering (all its
+        // workgroups at the same one): a running kernel holds up any call
+        // that waits for the device to drain (hipFree, hipHostFree, ...,
+        // from any thread), so a lane kept busy must still step aside; the
+        // host launches the next one behind it on the lane's stream
+        if (s_tag % reqs == 0)
+            break;
     }
-    if (t == 0)
-        __hip_atomic_store(&bell->exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == 0)   // (the launch's generation: a late store of an ended launch is not mistaken for this one's)
+        __hip_atomic_store(&bell->exited[g], gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Grid = `main_blocks` streaming blocks, then the edge blocks.
@@ -2429,9 +2561,12 @@ hipError_t launch_test_spin(hipStream_t s, uint32_t us)
     return hipGetLastError();
 }
 
-hipError_t launch_lane(hipStream_t s, LaneBell* bell, uint64_t idle_ticks)
+hipError_t launch_lane(hipStream_t s, LaneBell* bell, uint32_t workgroups, uint64_t idle_ticks, uint32_t gen,
+                       uint32_t reqs)
 {
-    k_lane<<<1, LANE_THREADS, 0, s>>>(bell, idle_ticks);
+    if (workgroups < 1 || workgroups > LANE_WGS_MAX || reqs == 0 || gen == 0)
+        return hipErrorInvalidValue;
+    k_lane<<<workgroups, LANE_THREADS, 0, s>>>(bell, idle_ticks, gen, reqs);
     return hipGetLastError();
 }
 

@@ -33,9 +33,14 @@
 
 #include "server/ws/ws.h"
 
+#include "wsg_capi.h"
+
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <cstring>
+#include <new>
+#include <type_traits>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -45,6 +50,75 @@
 
 namespace CppServer {
 namespace WS {
+
+//! A growable array of trivially copyable records in page-locked memory
+//! (wsg_host_alloc): a batch's frame table, records and descriptors, which
+//! the GPU pass then reads and writes where they are instead of through a
+//! staging copy.
+template <class T>
+class PinnedArray
+{
+    static_assert(std::is_trivially_copyable<T>::value, "PinnedArray holds plain records");
+
+public:
+    PinnedArray() = default;
+    PinnedArray(const PinnedArray&) = delete;
+    PinnedArray& operator=(const PinnedArray&) = delete;
+    PinnedArray(PinnedArray&& o) noexcept : _p(o._p), _n(o._n), _cap(o._cap) { o._p = nullptr, o._n = o._cap = 0; }
+    PinnedArray& operator=(PinnedArray&& o) noexcept
+    {
+        std::swap(_p, o._p);
+        std::swap(_n, o._n);
+        std::swap(_cap, o._cap);
+        return *this;
+    }
+    ~PinnedArray()
+    {
+        if (_p)
+            wsg_host_free(_p);
+    }
+    T* data() noexcept { return _p; }
+    const T* data() const noexcept { return _p; }
+    size_t size() const noexcept { return _n; }
+    bool empty() const noexcept { return _n == 0; }
+    void clear() noexcept { _n = 0; }
+    T& operator[](size_t i) noexcept { return _p[i]; }
+    const T& operator[](size_t i) const noexcept { return _p[i]; }
+    T* begin() noexcept { return _p; }
+    T* end() noexcept { return _p + _n; }
+    void push_back(const T& v)
+    {
+        if (_n == _cap)
+            grow(_n + 1);
+        _p[_n++] = v;
+    }
+    //! new elements are not initialized
+    void resize(size_t n)
+    {
+        if (n > _cap)
+            grow(n);
+        _n = n;
+    }
+
+private:
+    void grow(size_t need)
+    {
+        size_t cap = 2 * _cap > need ? 2 * _cap : need;
+        if (cap < 4096 / sizeof(T))
+            cap = 4096 / sizeof(T);
+        void* q = nullptr;
+        if (wsg_host_alloc(cap * sizeof(T), &q) != WSG_OK)
+            throw std::bad_alloc();
+        if (_n)
+            std::memcpy(q, _p, _n * sizeof(T));
+        if (_p)
+            wsg_host_free(_p);
+        _p = static_cast<T*>(q);
+        _cap = cap;
+    }
+    T* _p = nullptr;
+    size_t _n = 0, _cap = 0;
+};
 
 class WSReceiveBatch
 {
@@ -92,9 +166,9 @@ private:
     };
     struct Batch {
         Pinned wire, out;
-        std::vector<uint64_t> fs;
+        PinnedArray<uint64_t> fs;   // (page-locked: the decode pass reads the table and
         std::vector<Rec> recs;
-        std::vector<wsg_recv_info> info;
+        PinnedArray<wsg_recv_info> info;   //  writes the records in place)
         bool keyed = false;   // some frame carries a nonzero mask key: the GPU pass has bytes to change
         void reset()
         {
@@ -191,7 +265,7 @@ private:
 
     struct Queue_ {
         Pinned payload;
-        std::vector<wsg_send_desc> desc;
+        PinnedArray<wsg_send_desc> desc;   // (page-locked: read by the encode pass in place)
         std::vector<Rec> recs;
     };
 
@@ -199,7 +273,7 @@ private:
     std::vector<wsg_ctx*> _devs;   // SetDevices: owned, one per device
     Queue_ _q, _inflight;   // frames being queued | the frames a flush is encoding (written by its thread only)
     Pinned _wire;
-    std::vector<uint64_t> _wire_off;
+    PinnedArray<uint64_t> _wire_off;
     bool _flushing = false;
     std::thread::id _flusher;
     std::vector<std::pair<Transport*, void*>> _pending;   // other threads' Forget()s not applied yet

@@ -179,3 +179,133 @@ def test_lane_matches_launch_path_echo_shape(lane, launch):
     pin_in, pin_out = ca.pinned_empty(len(wire_o)), ca.pinned_empty(len(wire_o))
     for c in (lane, launch):
         _check_decode(c, pin_in, wire_o, off_o[:-1].copy(), pin_out)
+
+
+def test_lane_payload_arenas(lane):
+    """Encode reads its payloads from an LDS copy of the arena when the
+    arena's 16-B blocks fit LANE_PSTAGE (64 KiB), else from host memory: both
+    sides of that limit, arenas not 16-B aligned, frames scattered over a
+    large arena, and zero-length payloads, against the oracle."""
+    rng = np.random.default_rng(21)
+    big = ca.pinned_empty(1 << 19)
+    pin_w = ca.pinned_empty(1 << 17)
+    for arena in (0, 17, 65536 - 32, 65536 - 16, 65536 - 1, 65536, 65536 + 40, 300000):
+        for mis in (0, 1, 7, 15):
+            n = int(rng.integers(1, 1200))
+            lens = rng.integers(0, 60, n) if arena else np.zeros(n, np.int64)
+            lens = np.minimum(lens, arena)
+            desc = np.zeros(n, dtype=ca.SEND_DESC)
+            desc["len"] = lens
+            desc["src_off"] = [int(rng.integers(0, arena - int(ln) + 1)) for ln in lens]
+            # the first and last byte of the arena are read by some frame
+            if arena and n > 1 and lens[0] > 0:
+                desc["src_off"][0] = 0
+                desc["len"][-1] = min(int(lens[-1]) or 1, arena)
+                desc["src_off"][-1] = arena - int(desc["len"][-1])
+            desc["key"] = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+            desc["opcode"] = rng.choice(OPCODES, n)
+            desc["mask"] = rng.random(n) < 0.9
+            desc["status"] = np.where(rng.random(n) < 0.1, rng.integers(0, 70000, n), 0)
+            payload = wl.random_bytes(rng, arena)
+            view = big[mis: mis + arena]
+            view[:] = payload
+            wire_o, off_o = oracle.encode_batch(payload, desc)
+            assert len(wire_o) <= 65536
+            rc, wire, off = lane.encode_batch_host(view, desc, wire=pin_w)
+            assert rc == 0 and np.array_equal(off, off_o), (arena, mis)
+            assert np.array_equal(wire, wire_o), (arena, mis)
+
+
+@pytest.mark.parametrize("wgs", [1, 3, 16])
+def test_lane_workgroup_counts(wgs):
+    """The lane's workgroups ($WSG_LANE_WGS) split a request into frame
+    groups, each staged and written by one workgroup: one workgroup taking
+    several groups, an odd count, more workgroups than groups; decode in and
+    out of place, encode, against the oracle."""
+    c = _codec(WSG_LANE_MAX=65536, WSG_LANE_WGS=wgs)
+    try:
+        rng = np.random.default_rng(100 + wgs)
+        pin_p, pin_w = ca.pinned_empty(1 << 17), ca.pinned_empty(1 << 17)
+        pin_in, pin_out = ca.pinned_empty(1 << 17), ca.pinned_empty(1 << 17)
+        r0, _, _ = c.lane_stats()
+        for it in range(40):
+            if it % 4 == 0:   # many tiny frames: several groups per workgroup
+                n = int(rng.integers(2000, 4000))
+                desc, total = wl.ragged_desc(rng, rng.integers(0, 9, n))
+                desc["mask"] = True
+                payload = wl.random_bytes(rng, total + 16)
+            else:
+                payload, desc = _small_batch(rng)
+            wire_o, off_o = oracle.encode_batch(payload, desc)
+            pin_p[: len(payload)] = payload
+            rc, wire, off = c.encode_batch_host(pin_p[: len(payload)], desc, wire=pin_w)
+            assert rc == 0 and np.array_equal(off, off_o) and np.array_equal(wire, wire_o), (wgs, it)
+            fs = off_o[:-1].copy()
+            _check_decode(c, pin_in, wire_o, fs, pin_out)
+            _check_decode(c, pin_in, wire_o, fs)
+        r1, _, _ = c.lane_stats()
+        assert r1 - r0 >= 3 * 40 - 6, (r0, r1)
+    finally:
+        c.close()
+
+
+def test_lane_periodic_relaunch_and_device_sync():
+    """A launch of the lane ends after every $WSG_LANE_REQS-th request and
+    the next call launches it again behind it: results stay exact across the
+    hand-overs, and a device-wide synchronize from another thread (what
+    hipFree / hipHostFree do) waits for one hand-over, not for the busy lane
+    to go idle."""
+    import threading
+
+    c = _codec(WSG_LANE_MAX=65536, WSG_LANE_REQS=5)
+    busy = _codec(WSG_LANE_MAX=65536, WSG_LANE_REQS=64)
+    try:
+        rng = np.random.default_rng(17)
+        pin_in, pin_out = ca.pinned_empty(1 << 16), ca.pinned_empty(1 << 16)
+        r0, l0, _ = c.lane_stats()
+        for it in range(40):
+            payload, desc = _small_batch(rng, max_wire=30000)
+            wire_o, off_o = oracle.encode_batch(payload, desc)
+            _check_decode(c, pin_in, wire_o, off_o[:-1].copy(), pin_out)
+        r1, l1, _ = c.lane_stats()
+        assert r1 - r0 == 40 and l1 - l0 >= 7, (r1 - r0, l1 - l0)
+
+        # another thread keeps `busy`'s lane answering; this one synchronizes
+        payload, desc = _small_batch(np.random.default_rng(2), max_wire=30000)
+        wire_o, off_o = oracle.encode_batch(payload, desc)
+        fs = off_o[:-1].copy()
+        b_in, b_out = ca.pinned_empty(len(wire_o)), ca.pinned_empty(len(wire_o))
+        b_in[:] = wire_o
+        stop = threading.Event()
+        errors = []
+
+        def hammer():
+            try:
+                while not stop.is_set():
+                    rc, _, _ = busy.decode_batch_host(b_in, fs, out=b_out)
+                    if rc != 0:
+                        errors.append(rc)
+                        return
+            except Exception as e:  # pragma: no cover - reported below
+                errors.append(e)
+
+        th = threading.Thread(target=hammer)
+        th.start()
+        try:
+            time.sleep(0.3)
+            waits = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                torch.cuda.synchronize()
+                waits.append(time.perf_counter() - t0)
+                time.sleep(0.02)
+        finally:
+            stop.set()
+            th.join(timeout=30)
+        assert not th.is_alive() and not errors, errors
+        # one hand-over is 64 requests of tens of us; the idle limit alone
+        # would never come while the other thread keeps ringing
+        assert max(waits) < 0.25, waits
+    finally:
+        busy.close()
+        c.close()
