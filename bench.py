@@ -576,6 +576,20 @@ def echo_c1_leg(seconds=3.0, timeout=120):
             continue
         d = json.loads(r.stdout.strip().splitlines()[-1])
         out[leg] = {k: d[k] for k in ("msg_per_s", "MiB_per_s", "latency_ns", "total_messages", "payload_ok")}
+    # the same loop with the client's key 0 (tools/_build/echo_hostonly): no
+    # frame has a key, so no GPU pass runs; the API's host work alone (framing,
+    # delivery, queueing, hand-outs), i.e. what a per_read round costs besides
+    # its two GPU passes
+    ho = os.path.join(ROOT, "tools", "_build", "echo_hostonly")
+    if os.path.exists(ho):
+        r = _run_leg([ho, "per_read", "1", "1", "1000", "32", str(seconds)], timeout)
+        if r.returncode == 0:
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            out["host_only_1c"] = {k: d[k] for k in ("msg_per_s", "latency_ns", "payload_ok")}
+            out["host_only_1c"]["what"] = ("per_read_1c with client key 0: no GPU pass, the API's host work alone "
+                                           "(not a product mode: client keys are rand(), ws.cpp:97)")
+        else:
+            out["host_only_1c"] = {"error": (r.stderr or r.stdout).strip()[-300:]}
     # the reference's algorithm in the SAME loop: the oracle's restatement of
     # PrepareSendFrame / PrepareReceiveFrame (CPU, no GPU) driving the same
     # in-memory echo (tools/_build/bench_echo_ref; the cpu_baseline side)
@@ -1149,7 +1163,7 @@ def timed_region(w, steps, world, device):
     # interpreter's objects is a host stall of milliseconds, unrelated to the
     # path measured).  Not gc.collect() here: a collection right before t0
     # leaves the host's caches cold and adds ~100 us to a 20-step region
-    # (tools/gap3.py: wall - events 22 us without it, 119 us with it)
+    # (tools/region_gap.py: wall - events 22 us without it, 119 us with it)
     gc.disable()
     try:
         with marker("bench.%s.timed" % w.cfg):

@@ -1,7 +1,7 @@
 """bench.py's own C2 timed region (bench.timed_region on bench.Workload),
 repeated in one process: wall - events per region with the roctx range on
 and off, right after the oracle spot check and after a plain host pause.
-Diagnostic only.  usage: python tools/gap3.py [trials]
+Diagnostic only.  usage: python tools/region_gap.py [trials]
 """
 import contextlib
 import os
@@ -47,7 +47,7 @@ def main(trials):
     real_marker = bench.marker
     rows = {}
     def inline_region():
-        # gap2.py's region on the same workload: no barrier, gc or marker
+        # the bare region on the same workload: no barrier, gc or marker
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         e1.record()
