@@ -1052,8 +1052,21 @@ def fanout_many_leg(w, m=16, reps=10):
 
     fsz = ca.frame_size(0x82, True, length)
     bytes_out = m * k * fsz
+    # the bare write stream of the same bytes on the same buffer (torch's
+    # zero_: the runtime's fill), back to back like the calls above: the
+    # write-only ceiling the fan-out's stores run against
+    wire.zero_()
+    e0.record()
+    for _ in range(reps):
+        wire.zero_()
+    e1.record()
+    e1.synchronize()
+    fill_ms = e0.elapsed_time(e1) / reps
     return {"messages": m, "us_per_call": round(ms * 1e3, 2), "us_per_message": round(ms * 1e3 / m, 2),
-            "write_GBps": round(bytes_out / (ms * 1e-3) / 1e9, 1), "frame_bytes": fsz}
+            "write_GBps": round(bytes_out / (ms * 1e-3) / 1e9, 1), "frame_bytes": fsz,
+            "bare_write_stream": {"us": round(fill_ms * 1e3, 2), "write_GBps": round(bytes_out / (fill_ms * 1e-3) / 1e9, 1),
+                                  "fanout_vs_bare": round(fill_ms / ms, 4),
+                                  "what": "zero_() of the same bytes, back to back (the runtime's fill)"}}
 
 
 def c4_graph_leg(w, steps, reps=5):

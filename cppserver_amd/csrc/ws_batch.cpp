@@ -296,8 +296,7 @@ size_t WSReceiveBatch::Flush()
         // the payloads are handed out where they lie in the batch, at the
         // header sizes the framer recorded (b.info is not used)
     }
-    const bool keyed = b.keyed;
-    if (!keyed)
+    if (!b.keyed)
         payload_base = b.wire.p;
     size_t delivered = 0;
     const void* announced = nullptr;
@@ -326,17 +325,14 @@ size_t WSReceiveBatch::Flush()
             rec.ws->ResetMessage();
             continue;
         }
+        // the payload where the framer put it (its header size; the frames
+        // lie back to back), in the unmasked copy when a pass ran: the pass
+        // returned WSG_OK, so every frame parsed as framed and its record
+        // says the same (the records the GPU wrote are not read back)
         const size_t f = size_t(rec.frame);
-        if (keyed) {
-            const wsg_recv_info& in = b.info[f];
-            if (in.error)
-                throw std::runtime_error("WSReceiveBatch: decode rejected a framed frame");
-            rec.ws->DeliverFrame(rec.opcode, rec.fin, payload_base + in.payload_off, size_t(in.len));
-        } else {
-            const uint64_t at = b.fs[f] + rec.hdr;
-            const uint64_t end = f + 1 < n ? b.fs[f + 1] : b.wire.len;
-            rec.ws->DeliverFrame(rec.opcode, rec.fin, payload_base + at, size_t(end - at));
-        }
+        const uint64_t at = b.fs[f] + rec.hdr;
+        const uint64_t end = f + 1 < n ? b.fs[f + 1] : b.wire.len;
+        rec.ws->DeliverFrame(rec.opcode, rec.fin, payload_base + at, size_t(end - at));
         ++delivered;
     }
     return delivered;

@@ -1254,7 +1254,13 @@ int decode_host_direct(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const
             const auto t_back = std::chrono::steady_clock::now();
             if (info_dev != info)
                 std::memcpy(info, info_dev, size_t(n) * sizeof(wsg_recv_info));
-            const int rc = host_batch_status(c, wire, wire_len, frame_start, n, info);
+            // no frame erred (the lane's count): nothing for the status pass to
+            // find, and the records the GPU just wrote stay out of this core's
+            // caches unless the caller reads them
+            uint64_t errs = 0;
+            for (uint32_t g = 0; g < c->lane_wgs; ++g)
+                errs += lb->errs[g];
+            const int rc = errs ? host_batch_status(c, wire, wire_len, frame_start, n, info) : WSG_OK;
             if (c->lane_profile) {
                 using us = std::chrono::duration<double, std::micro>;
                 c->lane_prof[0] += us(t_ring - t_in).count();

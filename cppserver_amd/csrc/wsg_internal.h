@@ -129,6 +129,7 @@ struct LaneBell {
     LaneUnit w[LANE_WORDS];                // host: op | n << 32, a[0..5], G | profile << 32
     LaneUnit grp[LANE_GROUPS_MAX][2];      // host: group k's range (decode: wire [lo, hi); encode: payload span)
     uint64_t done[LANE_WGS_MAX];           // lane: workgroup g's last request answered (its tag, release)
+    uint64_t errs[LANE_WGS_MAX];           // lane: frames with an error among workgroup g's (decode; before done)
     uint64_t prof[8];                      // lane: workgroup 0's phase clocks ($WSG_LANE_PROFILE)
     uint32_t stop;                         // host: leave now
     uint32_t pad1[15];

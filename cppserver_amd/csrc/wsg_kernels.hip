@@ -1676,7 +1676,7 @@ __device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload,
 __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, uint64_t wire_len, uint64_t lo,
                                             uint64_t hi, const uint64_t* __restrict__ fs, uint32_t n, uint32_t f_lo,
                                             uint32_t cnt, uint8_t* out, wsg_recv_info* __restrict__ info,
-                                            uint8_t* lds, uint64_t* ts)
+                                            uint8_t* lds, uint64_t* ts, uint32_t* s_err)
 {
     v4u* s_wire = reinterpret_cast<v4u*>(lds);
     v4u* s_info = reinterpret_cast<v4u*>(lds + LANE_STAGE);                          // 2 blocks per record
@@ -1715,6 +1715,8 @@ __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, ui
         s_pl[t] = pl;
         s_pe[t] = e ? st : pl + r.len;
         s_key[t] = (e == 0 && r.masked) ? r.key : 0u;
+        if (e)
+            atomicAdd(s_err, 1u);   // (the host skips its status pass over the records when no frame erred)
     }
     __syncthreads();
     ts[1] = wall_clock64();
@@ -1779,6 +1781,7 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
     __shared__ uint64_t s_w[LANE_WORDS];
     __shared__ uint64_t s_g[LANE_GROUPS_PER_WG][2];
     __shared__ int s_go;
+    __shared__ uint32_t s_err;   // the request's frames with an error (decode)
     __shared__ v4u s_mem[LANE_LDS / 16];   // the op's staging (lane_decode / lane_encode layouts)
     const uint32_t t = threadIdx.x, g = blockIdx.x, nw = gridDim.x;
     uint64_t last = 0, seq = 0, t_seen = 0;
@@ -1853,6 +1856,7 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
             if (t == 0) {
                 s_go = go;
                 s_tag = seq;
+                s_err = 0;
             }
         }
         __syncthreads();
@@ -1872,7 +1876,7 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
             if (op == LANE_DECODE)
                 lane_decode(reinterpret_cast<const uint8_t*>(s_w[1]), s_w[2], s_g[j][0], s_g[j][1],
                             reinterpret_cast<const uint64_t*>(s_w[3]), n, f_lo, cnt, reinterpret_cast<uint8_t*>(s_w[4]),
-                            reinterpret_cast<wsg_recv_info*>(s_w[5]), lds, ts);
+                            reinterpret_cast<wsg_recv_info*>(s_w[5]), lds, ts, &s_err);
             else if (op == LANE_ENCODE)
                 lane_encode(reinterpret_cast<const uint8_t*>(s_w[1]), s_g[j][0], s_g[j][1],
                             reinterpret_cast<const wsg_send_desc*>(s_w[2]), f_lo, cnt,
@@ -1889,6 +1893,7 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
                 for (int k = 0; k < 5; ++k)
                     __hip_atomic_store(&bell->prof[k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
+            __hip_atomic_store(&bell->errs[g], uint64_t(s_err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&bell->done[g], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         last = seq;   // (wave 0's lanes: the tag they saw)
