@@ -5,7 +5,7 @@
 # rehearsal whose c5_job is now the C-ABI rank form.  Each step has its own
 # time limit; a fault / abort / time-out ends the script there.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/${TAG:-r4a}
 mkdir -p "$OUT"
 export TMPDIR=/tmp

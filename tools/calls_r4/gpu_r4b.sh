@@ -2,7 +2,7 @@
 # Round 4, second GPU call: the whole GPU suite on the new host paths, the
 # small-pass latency micro-benchmark (C1), the fan-out store-policy A/B.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/${TAG:-r4b}
 mkdir -p "$OUT"
 export TMPDIR=/tmp

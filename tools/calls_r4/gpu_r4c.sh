@@ -2,7 +2,7 @@
 # Round 4: the host lane — its tests, the fuzz suites of the host paths, the
 # C1 echo with and without it.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/${TAG:-r4c}
 mkdir -p "$OUT"
 export TMPDIR=/tmp

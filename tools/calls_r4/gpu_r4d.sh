@@ -1,7 +1,9 @@
 #!/bin/bash
+# Round 4: the lane after the relaxed poll; where its time goes (timing-only
+# builds); the lane tests; the echo.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/${TAG:-r4f}
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/${TAG:-r4d}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() {
@@ -17,7 +19,6 @@ step() {
 }
 step lane_tests 300 python -u -m pytest tests/test_gpu_lane.py -x -v --timeout 250 --timeout-method thread
 step lane_ab 300 python -u tools/lane_ab.py
+step lane_ab_4k 300 python -u tools/lane_ab.py 100 32 3000
 step echo_prof_1c 120 tools/_build/bench_echo_prof per_read 1 1 1000 32 3
-step echo_prof_100c 120 tools/_build/bench_echo_prof per_read 100 4 1000 32 3
-step host_suites 600 python -u -m pytest tests/test_gpu_fuzz.py tests/test_gpu_rx_batch.py tests/test_gpu_tx_batch.py tests/test_gpu_cpp_api.py tests/test_gpu_session.py tests/test_gpu_host_multi.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread
 echo "== done"

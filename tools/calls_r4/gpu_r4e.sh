@@ -1,6 +1,6 @@
 #!/bin/bash
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/${TAG:-r4e}
 mkdir -p "$OUT"
 export TMPDIR=/tmp

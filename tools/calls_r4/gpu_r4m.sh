@@ -3,7 +3,7 @@
 # SendAsync per run, scope sends without the connection's send lock) and the
 # host lane; the echo at 1c / 100c next to the host-only and reference loops.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/${TAG:-r4m}
 mkdir -p "$OUT"
 export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/bin/bash
 # 100 echo clients on 4 threads: tables in place vs copies, lane profile per context
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/${TAG:-r4q}
 mkdir -p "$OUT"
 export TMPDIR=/tmp

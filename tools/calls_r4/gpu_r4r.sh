@@ -1,7 +1,7 @@
 #!/bin/bash
 # Full GPU suite + smoke after the round-4 lane / host-path changes
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/${TAG:-r4r}
 mkdir -p "$OUT"
 export TMPDIR=/tmp

@@ -1,11 +1,11 @@
-"""Copy one tools/round_artifacts_r3.sh run into profiles/r3/: the bench line
+"""Copy one tools/round_artifacts.sh run into profiles/<round>/: the bench line
 as the driver runs it, the rocprofv3 kernel stats of the same command and
 its per-leg split (tools/trace_split.py), the PMC counter CSVs (codec
 kernels only) and the HBM traffic per launch they give
 (profiles/pmc_traffic.json via tools/pmc_summary.py, calibrated on the
 membench known-byte kernels of the same run).
 
-usage: python tools/collect_r3.py gpurun_out/art_r3
+usage: python tools/collect_round.py gpurun_out/art_r4 r4
 """
 import csv
 import glob
@@ -16,7 +16,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DST = os.path.join(ROOT, "profiles", "r3")
+DST = os.path.join(ROOT, "profiles", sys.argv[2] if len(sys.argv) > 2 else "r4")
 # pmc_traffic.json key -> (config run, kernel)
 KEYS = {"c2": ("c2", "k_decode"), "c3": ("c3", "k_encode_mask"), "c3_dec": ("c3", "k_decode"),
         "c4": ("c4", "k_fanout"), "c5": ("c5", "k_encode_mask")}

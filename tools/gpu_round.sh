@@ -8,4 +8,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 rc=$?; tail -3 gpurun_out/full/pytest.log; [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/full/smoke.log 2>&1 || exit $?
 tail -1 gpurun_out/full/smoke.log
-ROUND=${ROUND:-r1} bash tools/round_artifacts.sh
+ROUND=${ROUND:?set ROUND} bash tools/round_artifacts.sh
