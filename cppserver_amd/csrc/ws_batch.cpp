@@ -203,7 +203,7 @@ void WSReceiveBatch::Clear(WebSocket& ws)
 
 void WSReceiveBatch::Forget(WebSocket& ws)
 {
-    std::unique_lock<std::mutex> locker(_lock);
+    std::unique_lock<QueueLock> locker(_lock);
     for (Rec& r : _cur.recs)
         if (r.ws == &ws)
             r.ws = nullptr;
@@ -433,7 +433,7 @@ bool rec_matches(Transport* rt, void* rtag, Transport* transport, void* tag)
 
 void WSSendBatch::ForgetIf(Transport* transport, void* tag)
 {
-    std::unique_lock<std::mutex> locker(_lock);
+    std::unique_lock<QueueLock> locker(_lock);
     for (Rec& r : _q.recs)
         if (rec_matches(r.transport, r.tag, transport, tag))
             r = Rec{nullptr, nullptr, nullptr};

@@ -51,6 +51,37 @@
 namespace CppServer {
 namespace WS {
 
+//! The batches' queue lock.  Queueing a frame is a few stores, and an
+//! uncontended std::mutex — two locked instructions behind two libc calls per
+//! frame — was a fifth of a batched echo's host work (tools/sampler.cpp);
+//! this one is an inline exchange and a release store.  Contended (an
+//! explicit batch fed by several threads) it spins briefly, then yields.
+class QueueLock
+{
+public:
+    void lock() noexcept
+    {
+        for (unsigned i = 0; _held.exchange(true, std::memory_order_acquire); ++i) {
+            while (_held.load(std::memory_order_relaxed)) {
+                if (++i > 64)
+                    std::this_thread::yield();
+#if defined(__x86_64__)
+                else
+                    __builtin_ia32_pause();
+#endif
+            }
+        }
+    }
+    bool try_lock() noexcept
+    {
+        return !_held.load(std::memory_order_relaxed) && !_held.exchange(true, std::memory_order_acquire);
+    }
+    void unlock() noexcept { _held.store(false, std::memory_order_release); }
+
+private:
+    std::atomic<bool> _held{false};
+};
+
 //! A growable array of trivially copyable records in page-locked memory
 //! (wsg_host_alloc): a batch's frame table, records and descriptors, which
 //! the GPU pass then reads and writes where they are instead of through a
@@ -193,10 +224,10 @@ private:
     std::atomic<bool> _has_pending{false};
     std::atomic<const void*> _busy{nullptr};   // the connection the flush is at (announced before its Forget check)
     std::atomic<int> _waiters{0};              // Forget()s waiting for _busy to move on
-    std::condition_variable _busy_cv;
+    std::condition_variable_any _busy_cv;
     std::atomic<size_t> _n_frames{0};          // _cur.fs.size(), written under _lock
     std::atomic<uint64_t> _n_bytes{0};         // _cur.wire.len, written under _lock
-    mutable std::mutex _lock;   // _cur, _flushing, _pending
+    mutable QueueLock _lock;   // _cur, _flushing, _pending
 };
 
 class Transport;
@@ -280,7 +311,7 @@ private:
     std::atomic<bool> _has_pending{false};
     std::atomic<const void*> _busy{nullptr};   // transport / tag the flush is at (see WSReceiveBatch)
     std::atomic<int> _waiters{0};
-    std::condition_variable _busy_cv;
+    std::condition_variable_any _busy_cv;
     std::atomic<size_t> _n_frames{0};   // _q.desc.size(), written under _lock
     std::atomic<uint64_t> _n_bytes{0};  // _q.payload.len, written under _lock
     void Counted()
@@ -288,7 +319,7 @@ private:
         _n_frames.store(_q.desc.size(), std::memory_order_relaxed);
         _n_bytes.store(_q.payload.len, std::memory_order_relaxed);
     }
-    mutable std::mutex _lock;   // _q, _flushing, _pending
+    mutable QueueLock _lock;   // _q, _flushing, _pending
 };
 
 /*
