@@ -64,9 +64,17 @@ uint32_t le32(const uint8_t k[4])
 
 } // namespace
 
+// The library's thread_locals use the initial-exec TLS model: a direct
+// thread-pointer access.  Under the default model each access calls
+// __tls_get_addr, and with glibc before 2.39 every call took its slow path
+// once a later dlopen (the HIP runtime's) had raised the TLS generation: 8-9 %
+// of a batched echo's host time (tools/sampler.cpp).  The library's TLS is
+// 113 bytes, well inside the static TLS a dlopen (ctypes) may still take.
+#define WSG_TLS __attribute__((tls_model("initial-exec")))
+
 wsg_ctx* ThreadCodec()
 {
-    thread_local ThreadCtx holder;
+    thread_local ThreadCtx holder WSG_TLS;
     if (!holder.ctx) {
         const char* dev = std::getenv("WSG_DEVICE");
         check(wsg_create(dev ? std::atoi(dev) : 0, &holder.ctx), "wsg_create");
@@ -399,7 +407,7 @@ void WebSocket::ClearWSBuffers()
 // C-ABI sessions (include/wsg_capi.h)
 // ===========================================================================
 
-thread_local wsg_rx_dispatch g_rx_dispatch;
+thread_local wsg_rx_dispatch g_rx_dispatch WSG_TLS;
 
 extern "C" {
 

@@ -674,7 +674,7 @@ struct AutoState {
 
 AutoState& auto_state()
 {
-    thread_local AutoState st;
+    thread_local AutoState st __attribute__((tls_model("initial-exec")));   // (see ThreadCodec, ws.cpp)
     if (st.enabled < 0) {
         const char* e = std::getenv("WSG_AUTO_BATCH");
         st.enabled = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
