@@ -1212,6 +1212,30 @@ def timed_region(w, steps, world, device):
             "minmax": spread, "submit_ms": (t_sub - t0) * 1e3}
 
 
+# CPU baselines run after every GPU leg and host leg: a baseline loads every
+# core for seconds, and the legs timed right after it ran slower (a C4
+# region 12.6 us per launch after C3's 16-thread baseline against 8.0 us
+# with none before it, profiles/r4/c4_after_cpu_baseline.log)
+_DEFERRED_CPU = []
+
+
+def defer_cpu_baseline(obj, w, seconds):
+    import types
+
+    snap = types.SimpleNamespace(cfg=w.cfg, host=w.host, payload_bytes=w.payload_bytes,
+                                 length=getattr(w, "length", None))
+    _DEFERRED_CPU.append((obj, snap, seconds))
+
+
+def run_deferred_cpu_baselines(cpu):
+    while _DEFERRED_CPU:
+        obj, snap, seconds = _DEFERRED_CPU.pop(0)
+        try:
+            obj["cpu_baseline"], obj["cpu_baseline_mt"] = cpu_baseline(snap, seconds, cpu)
+        except Exception as e:   # noqa: BLE001  (reported; the GPU numbers stand)
+            obj["cpu_baseline"] = {"error": repr(e)[:300]}
+
+
 def config_obj(args, cfg, codec, rank, world, device, steps, warmup, cpu):
     """One BASELINE config measured in this run: its own workload, spot check
     against the oracle, warm-up, timed region, roofline per dominant kernel
@@ -1261,8 +1285,8 @@ def config_obj(args, cfg, codec, rank, world, device, steps, warmup, cpu):
             many["frac"] = round(per_msg / (many["us_per_message"] * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
             obj["multicast_tick_16"] = many
         if cpu is not None and rank == 0:
-            c1, cn = cpu_baseline(w, args.cpu_seconds * 0.6, cpu)
-            obj["cpu_baseline"], obj["cpu_baseline_mt"] = c1, cn
+            # timed at the end of the run (defer_cpu_baseline)
+            defer_cpu_baseline(obj, w, args.cpu_seconds * 0.6)
         obj["spot_check"] = ok
         return obj
     finally:
@@ -1412,9 +1436,9 @@ def main():
             if capi is not None:
                 extras["c5_job_one_process"] = capi
     cpu = host_cpu() if (rank == 0 and world == 1 and not args.no_cpu) else None
-    cpu1 = cpu_mt = None
+    headline_cpu = {}
     if cpu is not None:
-        cpu1, cpu_mt = cpu_baseline(w, args.cpu_seconds, cpu)
+        defer_cpu_baseline(headline_cpu, w, args.cpu_seconds)
     if rank == 0 and world == 1 and not args.no_extras:
         extras["copy_ceiling_GBps"] = round(copy_ceiling(w), 1)
         pc = pcie_inclusive(w)
@@ -1455,6 +1479,9 @@ def main():
         mc = multicast_leg()
         if mc is not None:
             extras["ws_multicast"] = mc
+    if cpu is not None:
+        run_deferred_cpu_baselines(cpu)
+    cpu1, cpu_mt = headline_cpu.get("cpu_baseline"), headline_cpu.get("cpu_baseline_mt")
 
     if world > 1:
         import torch.distributed as dist
