@@ -406,8 +406,20 @@ int lane_start(wsg_ctx* c)
             return WSG_ENOMEM;
         std::memset(p, 0, sizeof(wsg::LaneBell));
         c->lane.bell = static_cast<wsg::LaneBell*>(p);
-        if (hipStreamCreateWithFlags(&c->lane.stream, hipStreamNonBlocking) != hipSuccess)
+        // A running lane holds the hardware queue its stream is on: every
+        // packet queued behind it waits until the launch ends.  The runtime
+        // keeps streams of each priority on their own queues, so the lanes
+        // go on high-priority streams (ahead of nothing but other lanes) and
+        // the contexts' ordinary streams never queue behind one
+        // ($WSG_LANE_PRIORITY=0: the default priority, A/B)
+        int lo = 0, hi = 0;
+        const char* pe = std::getenv("WSG_LANE_PRIORITY");
+        if ((!pe || *pe != '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
+            if (hipStreamCreateWithPriority(&c->lane.stream, hipStreamNonBlocking, hi) != hipSuccess)
+                return WSG_EHIP;
+        } else if (hipStreamCreateWithFlags(&c->lane.stream, hipStreamNonBlocking) != hipSuccess) {
             return WSG_EHIP;
+        }
         static std::once_flag once;
         std::call_once(once, [] { std::atexit(lanes_at_exit); });
         std::lock_guard<std::mutex> g(lane_registry_lock());
