@@ -6,6 +6,7 @@
 #include "wsg_trace.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -114,12 +115,14 @@ struct wsg_ctx {
         hipStream_t stream = nullptr;
         bool running = false;            // launched, not yet seen leaving
         bool broken = false;             // did not answer: the launch paths from now on
+        bool declined = false;           // the process already holds lane_cap lanes: the launch paths
         uint64_t seq = 0;
         uint64_t launches = 0;           // kernel launches of the lane (wsg_lane_stats)
         uint32_t gen = 0;                // the running launch's number (exited[] holds it when it leaves)
     } lane;
     uint64_t lane_max = 64 << 10;
     uint32_t lane_wgs = 8;          // workgroups (CUs) sharing a request's reads and writes
+    int lane_cap = 4;               // this context takes a lane only while the process holds fewer ($WSG_LANE_CAP)
     bool tables_in_place = true;    // the direct paths use tables in wsg_host_alloc blocks in place ($WSG_TABLES_IN_PLACE, A/B)
     uint32_t lane_idle_us = 2000;   // the lane leaves after this long without a request
     uint32_t lane_reqs = 256;       // ... and after every lane_reqs-th request ($WSG_LANE_REQS)
@@ -522,12 +525,37 @@ int lane_call(wsg_ctx* c, uint32_t op, uint32_t n, uint32_t G, const uint64_t (&
     }
 }
 
+// Contexts of this process holding a lane (its doorbell allocated), and the
+// most it lets hold one ($WSG_LANE_CAP, default 4).  Every lane's
+// workgroups poll host memory over PCIe; with eight lanes (a TCP echo's four
+// server and four client threads) the polls cost more than the launches
+// they save: 100 clients 23.5 M msg/s with a lane per context, 30.3 M with
+// four, 39.4 M with none; one client 9.5 / 9.2 / 6.2 M; in memory, 100
+// clients on 4 threads 43.7 / 43.8 / 28.8 M (profiles/r4/lane_cap_ab.log).
+std::atomic<int>& lane_holders()
+{
+    static std::atomic<int> n{0};
+    return n;
+}
+
 // The lane for a request, launched if it is not running; nullptr when it
-// cannot be used (it did not answer before, or its launch failed).
+// cannot be used (it did not answer before, its launch failed, or the
+// process holds its cap of lanes already).
 wsg::LaneBell* lane_ready(wsg_ctx* c)
 {
-    if (c->lane.broken || lane_start(c) != WSG_OK)
+    if (c->lane.broken || c->lane.declined)
         return nullptr;
+    const bool fresh = !c->lane.bell;
+    if (fresh && lane_holders().fetch_add(1) >= c->lane_cap) {
+        lane_holders().fetch_sub(1);
+        c->lane.declined = true;
+        return nullptr;
+    }
+    if (lane_start(c) != WSG_OK) {
+        if (fresh && !c->lane.bell)
+            lane_holders().fetch_sub(1);
+        return nullptr;
+    }
     return c->lane.bell;
 }
 
@@ -535,6 +563,7 @@ void lane_release(wsg_ctx* c)
 {
     if (!c->lane.bell)
         return;
+    lane_holders().fetch_sub(1);
     {
         std::lock_guard<std::mutex> g(lane_registry_lock());
         auto& reg = lane_registry();
@@ -638,6 +667,11 @@ int wsg_create(int device, wsg_ctx** out)
         c->lane_max = std::strtoull(e, nullptr, 10);
     if (const char* e = std::getenv("WSG_LANE_PROFILE"))
         c->lane_profile = *e == '1';
+    if (const char* e = std::getenv("WSG_LANE_CAP")) {
+        const long v = std::atol(e);
+        if (v >= 1 && v <= (1l << 20))
+            c->lane_cap = int(v);
+    }
     if (const char* e = std::getenv("WSG_LANE_REQS")) {
         const long v = std::atol(e);
         if (v >= 1 && v <= (1l << 30))

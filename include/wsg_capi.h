@@ -336,13 +336,17 @@ int wsg_timing_minmax(wsg_ctx* ctx, double* min_ms, double* max_ms);
 
 /* ---- the host lane (measurement / test hook) ----------------------------- */
 /* Page-locked host batches of at most $WSG_LANE_MAX wire bytes (default 64
- * KiB) whose frame table is strictly increasing go to a resident
- * one-workgroup kernel of the context through a doorbell in host memory
- * instead of a launch and a synchronize per call (the C1 echo's reads).  It
- * leaves after $WSG_LANE_IDLE_US (default 2000) without a request and is
- * launched again on the next.  Requests it answered, its launches, and
- * whether it runs now (1), has left (0) or stopped answering (-1: the
- * launch paths from then on).                                               */
+ * KiB) whose frame table is strictly increasing go to a resident kernel of
+ * the context ($WSG_LANE_WGS workgroups, default 8, on a high-priority
+ * stream) through a doorbell in host memory instead of a launch and a
+ * synchronize per call (the C1 echo's reads).  A launch ends after
+ * $WSG_LANE_IDLE_US (default 2000) without a request and after every
+ * $WSG_LANE_REQS-th request (default 256: a running kernel holds up calls
+ * that wait for the device to drain), and the next call launches it again.
+ * At most $WSG_LANE_CAP contexts of a process (default 4) hold a lane; the
+ * others take the launch paths.
+ * Requests it answered, its launches, and whether it runs now (1), has left
+ * (0) or stopped answering (-1: the launch paths from then on).            */
 int wsg_lane_stats(wsg_ctx* ctx, uint64_t* requests, uint64_t* launches, int* running);
 
 #ifdef __cplusplus

@@ -31,6 +31,10 @@ OPCODES = [0x81, 0x82, 0x01, 0x88, 0x89, 0x8A, 0xC2]
 
 
 def _codec(**env):
+    # every lane test's context takes a lane whatever other tests of this
+    # process hold ($WSG_LANE_CAP bounds a process's lanes; its own test
+    # below)
+    env.setdefault("WSG_LANE_CAP", 1000)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update({k: str(v) for k, v in env.items()})
     try:
@@ -309,3 +313,26 @@ def test_lane_periodic_relaunch_and_device_sync():
     finally:
         busy.close()
         c.close()
+
+
+def test_lane_cap_declines_extra_contexts():
+    """At most $WSG_LANE_CAP contexts of a process hold a lane: a context
+    created with a cap the process already meets takes the launch paths
+    (no lane request, same bytes); a lane's holder closing frees its place."""
+    rng = np.random.default_rng(23)
+    payload, desc = _small_batch(rng, max_wire=20000)
+    wire_o, off_o = oracle.encode_batch(payload, desc)
+    fs = off_o[:-1].copy()
+    pin_in, pin_out = ca.pinned_empty(1 << 16), ca.pinned_empty(1 << 16)
+    a = _codec(WSG_LANE_MAX=65536)
+    try:
+        _check_decode(a, pin_in, wire_o, fs, pin_out)
+        assert a.lane_stats()[0] == 1
+        b = _codec(WSG_LANE_MAX=65536, WSG_LANE_CAP=1)   # the process holds >= 1 lane (a's)
+        try:
+            _check_decode(b, pin_in, wire_o, fs, pin_out)
+            assert b.lane_stats()[:2] == (0, 0)
+        finally:
+            b.close()
+    finally:
+        a.close()

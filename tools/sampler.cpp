@@ -3,8 +3,8 @@
 // the interrupted instruction address; at exit the samples are written as
 // "module offset count" lines (to $WSG_SAMPLER_OUT, default sampler.txt) for
 // tools/sampler_report.py to symbolize with addr2line. Enabled by setting
-// $WSG_SAMPLER (the period in microseconds, e.g. 200).  $WSG_CRASH_TRACE=1:
-// a backtrace on a host crash (SIGSEGV / SIGABRT) to stderr.
+// $WSG_SAMPLER (the period in microseconds, e.g. 200).  A host crash
+// (SIGSEGV / SIGABRT) prints a backtrace to stderr ($WSG_CRASH_TRACE=0: not).
 #include <execinfo.h>
 #include <signal.h>
 #include <unistd.h>
@@ -119,7 +119,8 @@ void on_crash(int sig)
 
 struct Start {
     Start() {
-        if (std::getenv("WSG_CRASH_TRACE")) {   // a backtrace on SIGSEGV / SIGABRT (host code)
+        const char* ct = std::getenv("WSG_CRASH_TRACE");
+        if (!ct || *ct != '0') {   // a backtrace on SIGSEGV / SIGABRT (host code); $WSG_CRASH_TRACE=0: off
             signal(SIGSEGV, on_crash);
             signal(SIGABRT, on_crash);
         }
