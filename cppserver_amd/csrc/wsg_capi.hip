@@ -417,10 +417,13 @@ int lane_start(wsg_ctx* c)
         // ($WSG_LANE_PRIORITY=0: the default priority, A/B)
         int lo = 0, hi = 0;
         const char* pe = std::getenv("WSG_LANE_PRIORITY");
-        if ((!pe || *pe != '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
-            if (hipStreamCreateWithPriority(&c->lane.stream, hipStreamNonBlocking, hi) != hipSuccess)
-                return WSG_EHIP;
-        } else if (hipStreamCreateWithFlags(&c->lane.stream, hipStreamNonBlocking) != hipSuccess) {
+        const bool made = (!pe || *pe != '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess
+                              ? hipStreamCreateWithPriority(&c->lane.stream, hipStreamNonBlocking, hi) == hipSuccess
+                              : hipStreamCreateWithFlags(&c->lane.stream, hipStreamNonBlocking) == hipSuccess;
+        if (!made) {   // (never a launch on the null stream: the doorbell goes, the next call tries again)
+            c->lane.stream = nullptr;
+            (void)hipHostFree(p);
+            c->lane.bell = nullptr;
             return WSG_EHIP;
         }
         static std::once_flag once;
