@@ -7,6 +7,7 @@
 // the gfx950 kernel behind wsg_xor_host.  Reference semantics followed:
 // source/server/ws/ws.cpp:212-498, including the quirks of SURVEY.md §8a.
 #include "server/ws/ws.h"
+#include "wsg_env.h"
 #include "server/ws/ws_handshake.h"
 #include "ws_session_impl.h"
 
@@ -76,7 +77,7 @@ wsg_ctx* ThreadCodec()
 {
     thread_local ThreadCtx holder WSG_TLS;
     if (!holder.ctx) {
-        const char* dev = std::getenv("WSG_DEVICE");
+        const char* dev = wsg::envp("WSG_DEVICE");
         check(wsg_create(dev ? std::atoi(dev) : 0, &holder.ctx), "wsg_create");
     }
     return holder.ctx;

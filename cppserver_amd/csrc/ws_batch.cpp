@@ -7,6 +7,7 @@
 // message half (ws.cpp:407-452) WebSocket::DeliverFrame, called in arrival
 // order.
 #include "server/ws/ws_batch.h"
+#include "wsg_env.h"
 #include "server/ws/ws_transport.h"
 #include "ws_session_impl.h"
 #include "wsg_frame.h"
@@ -676,7 +677,7 @@ AutoState& auto_state()
 {
     thread_local AutoState st __attribute__((tls_model("initial-exec")));   // (see ThreadCodec, ws.cpp)
     if (st.enabled < 0) {
-        const char* e = std::getenv("WSG_AUTO_BATCH");
+        const char* e = wsg::envp("WSG_AUTO_BATCH");
         st.enabled = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
     }
     return st;

@@ -3,6 +3,7 @@
 // Nothing here computes payload bytes on the CPU: every payload byte of
 // every entry point is produced by a gfx950 kernel.
 #include "wsg_internal.h"
+#include "wsg_env.h"
 #include "wsg_trace.h"
 
 #include <algorithm>
@@ -302,7 +303,7 @@ namespace {
 unsigned host_alloc_flags()
 {
     static const unsigned f = [] {
-        const char* e = std::getenv("WSG_HOST_COHERENT");
+        const char* e = wsg::envp("WSG_HOST_COHERENT");
         return (e && *e == '1') ? unsigned(hipHostMallocCoherent | hipHostMallocMapped) : unsigned(hipHostMallocDefault);
     }();
     return f;
@@ -328,21 +329,42 @@ void host_blocks_add(const void* p, uint64_t bytes)
     std::lock_guard<std::mutex> g(host_blocks_lock());
     host_blocks()[reinterpret_cast<uintptr_t>(p)] = bytes;
 }
+// Bumped by every removal: a thread's cached blocks (in_host_block) are
+// trusted only while it is unchanged.
+std::atomic<uint64_t> g_blocks_gen{0};
 void host_blocks_remove(const void* p)
 {
     std::lock_guard<std::mutex> g(host_blocks_lock());
     host_blocks().erase(reinterpret_cast<uintptr_t>(p));
+    g_blocks_gen.fetch_add(1, std::memory_order_release);
 }
+// Each host call checks several pointers (wire, output, table, records):
+// under one process-wide lock, eight IO threads queued on it; a thread
+// remembers the last blocks it found, valid until a block is removed.
+struct BlockHit {
+    uintptr_t base = 0;
+    uint64_t size = 0;
+    uint64_t gen = ~uint64_t(0);
+};
+thread_local BlockHit t_hits[4] __attribute__((tls_model("initial-exec")));
+thread_local uint32_t t_hit_next __attribute__((tls_model("initial-exec"))) = 0;
 bool in_host_block(const void* p, uint64_t bytes = 1)
 {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint64_t gen = g_blocks_gen.load(std::memory_order_acquire);
+    for (const BlockHit& h : t_hits)
+        if (h.gen == gen && a - h.base < h.size && bytes <= h.size - (a - h.base))
+            return true;
     std::lock_guard<std::mutex> g(host_blocks_lock());
     auto& m = host_blocks();
     auto it = m.upper_bound(a);
     if (it == m.begin())
         return false;
     --it;
-    return a - it->first < it->second && bytes <= it->second - (a - it->first);
+    if (!(a - it->first < it->second && bytes <= it->second - (a - it->first)))
+        return false;
+    t_hits[t_hit_next++ & 3] = BlockHit{it->first, it->second, gen};
+    return true;
 }
 
 } // namespace
@@ -416,7 +438,7 @@ int lane_start(wsg_ctx* c)
         // the contexts' ordinary streams never queue behind one
         // ($WSG_LANE_PRIORITY=0: the default priority, A/B)
         int lo = 0, hi = 0;
-        const char* pe = std::getenv("WSG_LANE_PRIORITY");
+        const char* pe = wsg::envp("WSG_LANE_PRIORITY");
         const bool made = (!pe || *pe != '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess
                               ? hipStreamCreateWithPriority(&c->lane.stream, hipStreamNonBlocking, hi) == hipSuccess
                               : hipStreamCreateWithFlags(&c->lane.stream, hipStreamNonBlocking) == hipSuccess;
@@ -588,6 +610,22 @@ extern "C" {
 
 int wsg_abi_version(void) { return WSG_ABI_VERSION; }
 
+}   // extern "C"
+
+// The runtime's first initialization under the environment lock (wsg_env.h):
+// every entry point that can be a process's first HIP call goes through here
+// before touching HIP or reading a knob.
+void wsg::hip_init_once()
+{
+    static std::once_flag once;
+    std::call_once(once, [] {
+        std::lock_guard<std::recursive_mutex> g(wsg::env_mutex());
+        (void)hipInit(0);
+    });
+}
+
+extern "C" {
+
 const char* wsg_strerror(int code)
 {
     switch (code) {
@@ -612,6 +650,8 @@ int wsg_create(int device, wsg_ctx** out)
     if (!out)
         return WSG_EINVAL;
     *out = nullptr;
+    wsg::hip_init_once();
+    std::lock_guard<std::recursive_mutex> env_guard(wsg::env_mutex());   // (wsg_env.h)
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || device < 0 || device >= count)
         return WSG_EHIP;
@@ -631,63 +671,63 @@ int wsg_create(int device, wsg_ctx** out)
         return WSG_EHIP;
     }
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    if (const char* e = std::getenv("WSG_BLOCKS_PER_CU")) {
+    if (const char* e = wsg::envp("WSG_BLOCKS_PER_CU")) {
         const int v = std::atoi(e);
         if (v > 0 && v <= 4096)
             c->blocks_per_cu = c->dec_blocks_per_cu = c->enc_blocks_per_cu = v;   // A/B runs: every grid
     }
-    if (const char* e = std::getenv("WSG_XOR_DIRECT_MAX"))   // A/B measurements (per-call path)
+    if (const char* e = wsg::envp("WSG_XOR_DIRECT_MAX"))   // A/B measurements (per-call path)
         c->xor_direct_max = std::strtoull(e, nullptr, 10);
-    if (const char* e = std::getenv("WSG_HOST_DIRECT_MAX"))   // A/B measurements (small host batches)
+    if (const char* e = wsg::envp("WSG_HOST_DIRECT_MAX"))   // A/B measurements (small host batches)
         c->host_direct_max = std::strtoull(e, nullptr, 10);
-    if (const char* e = std::getenv("WSG_DEC_TILES_PER_BLOCK")) {   // A/B measurements (tools/tune.py)
+    if (const char* e = wsg::envp("WSG_DEC_TILES_PER_BLOCK")) {   // A/B measurements (tools/tune.py)
         const int v = std::atoi(e);
         if (v >= 0 && v <= 64)
             c->dec_tiles_per_block = v;
     }
-    if (const char* e = std::getenv("WSG_CHECK"))   // debug: checked launches (see in_alloc)
+    if (const char* e = wsg::envp("WSG_CHECK"))   // debug: checked launches (see in_alloc)
         c->check = *e == '1';
-    if (const char* e = std::getenv("WSG_ENC_BLOCKS_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
+    if (const char* e = wsg::envp("WSG_ENC_BLOCKS_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
         const int v = std::atoi(e);
         if (v > 0 && v <= 32768)
             c->enc_blocks_per_cu = v;
     }
-    if (const char* e = std::getenv("WSG_ENC_LAUNCH_PIECES"))   // A/B measurements (tools/c5_split.py)
+    if (const char* e = wsg::envp("WSG_ENC_LAUNCH_PIECES"))   // A/B measurements (tools/c5_split.py)
         c->enc_launch_pieces = std::strtoull(e, nullptr, 10);
-    if (const char* e = std::getenv("WSG_FAN_WPB")) {   // A/B measurements (tools/c4_ab.py)
+    if (const char* e = wsg::envp("WSG_FAN_WPB")) {   // A/B measurements (tools/c4_ab.py)
         const int v = std::atoi(e);
         if (v == 1 || v == 2 || v == 4 || v == 8 || v == 16)
             c->fan_wpb = v;
     }
-    if (const char* e = std::getenv("WSG_FAN_WAVES_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
+    if (const char* e = wsg::envp("WSG_FAN_WAVES_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
         const int v = std::atoi(e);
         if (v > 0 && v <= 64)
             c->fan_waves_per_cu = v;
     }
-    if (const char* e = std::getenv("WSG_SMALL_AVG"))   // A/B measurements (tools/tune_enc.py)
+    if (const char* e = wsg::envp("WSG_SMALL_AVG"))   // A/B measurements (tools/tune_enc.py)
         c->small_avg = std::strtoull(e, nullptr, 10);
-    if (const char* e = std::getenv("WSG_LANE_MAX"))   // A/B measurements (tools/echo_size.py, bench_echo)
+    if (const char* e = wsg::envp("WSG_LANE_MAX"))   // A/B measurements (tools/echo_size.py, bench_echo)
         c->lane_max = std::strtoull(e, nullptr, 10);
-    if (const char* e = std::getenv("WSG_LANE_PROFILE"))
+    if (const char* e = wsg::envp("WSG_LANE_PROFILE"))
         c->lane_profile = *e == '1';
-    if (const char* e = std::getenv("WSG_LANE_CAP")) {
+    if (const char* e = wsg::envp("WSG_LANE_CAP")) {
         const long v = std::atol(e);
         if (v >= 1 && v <= (1l << 20))
             c->lane_cap = int(v);
     }
-    if (const char* e = std::getenv("WSG_LANE_REQS")) {
+    if (const char* e = wsg::envp("WSG_LANE_REQS")) {
         const long v = std::atol(e);
         if (v >= 1 && v <= (1l << 30))
             c->lane_reqs = uint32_t(v);
     }
-    if (const char* e = std::getenv("WSG_TABLES_IN_PLACE"))
+    if (const char* e = wsg::envp("WSG_TABLES_IN_PLACE"))
         c->tables_in_place = *e != '0';
-    if (const char* e = std::getenv("WSG_LANE_WGS")) {
+    if (const char* e = wsg::envp("WSG_LANE_WGS")) {
         const long v = std::atol(e);
         if (v >= 1 && v <= long(wsg::LANE_WGS_MAX))
             c->lane_wgs = uint32_t(v);
     }
-    if (const char* e = std::getenv("WSG_LANE_IDLE_US")) {
+    if (const char* e = wsg::envp("WSG_LANE_IDLE_US")) {
         const long v = std::atol(e);
         if (v > 0 && v <= 1000000)
             c->lane_idle_us = uint32_t(v);
@@ -1115,7 +1155,7 @@ struct Pipe {
 
 int pipe_for(wsg_ctx* c, wsg_ctx::Slot& sl, Pipe& p)
 {
-    const char* e = std::getenv("WSG_PIPE");
+    const char* e = wsg::envp("WSG_PIPE");
     p.roles = !(e && std::strcmp(e, "slots") == 0);
     if (!p.roles) {
         p.h2d = p.kern = p.d2h = sl.stream;
@@ -1212,6 +1252,7 @@ int wsg_host_alloc(size_t bytes, void** out)
     if (!out)
         return WSG_EINVAL;
     *out = nullptr;
+    wsg::hip_init_once();
     if (hipHostMalloc(out, bytes ? bytes : 1, host_alloc_flags()) != hipSuccess)
         return WSG_ENOMEM;
     host_blocks_add(*out, bytes ? bytes : 1);
@@ -1344,7 +1385,7 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
             return WSG_OK;
         }
         uint64_t seg_bytes = 32ull << 20;
-        if (const char* e = std::getenv("WSG_STAGE_MB"))
+        if (const char* e = wsg::envp("WSG_STAGE_MB"))
             seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
         const bool in_pinned = host_pinned(wire), out_pinned = host_pinned(out);
         if (in_pinned && out_pinned && wire_len <= c->host_direct_max && aligned16(wire) && aligned16(out) &&
@@ -1506,7 +1547,7 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
         if (n == 0)
             return WSG_OK;
         uint64_t seg_bytes = 32ull << 20;
-        if (const char* e = std::getenv("WSG_STAGE_MB"))
+        if (const char* e = wsg::envp("WSG_STAGE_MB"))
             seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
         const bool in_pinned = host_pinned(payload), out_pinned = host_pinned(wire);
         if (in_pinned && out_pinned && wire_off[n] <= c->host_direct_max && aligned16(wire) && n <= (1u << 20) &&

@@ -24,6 +24,7 @@
 // ROCm install, so that a host process which already carries another RCCL
 // (PyTorch bundles one) keeps the two apart.
 #include "wsg_internal.h"
+#include "wsg_env.h"
 #include "wsg_trace.h"
 
 #include <rccl/rccl.h>
@@ -59,7 +60,7 @@ const Rccl* rccl()
     static Rccl r;
     static std::once_flag once;
     std::call_once(once, [] {
-        const char* names[] = {std::getenv("WSG_RCCL_LIB"), "/opt/rocm/lib/librccl.so.1", "librccl.so.1",
+        const char* names[] = {wsg::envp("WSG_RCCL_LIB"), "/opt/rocm/lib/librccl.so.1", "librccl.so.1",
                                "librccl.so"};
         for (const char* n : names) {
             if (!n || !*n)
@@ -107,7 +108,7 @@ const Rccl* rccl()
 uint32_t test_null_spin_us()
 {
     static const uint32_t us = [] {
-        const char* e = std::getenv("WSG_TEST_NULL_SPIN_US");
+        const char* e = wsg::envp("WSG_TEST_NULL_SPIN_US");
         return e ? uint32_t(std::strtoul(e, nullptr, 10)) : 0u;
     }();
     return us;
@@ -228,7 +229,7 @@ void on_contexts(wsg_ctx* const* ctxs, int parts, Fn fn)
 // context (the one-GPU tests exercise the split that way).
 std::vector<wsg_ctx*> one_per_device(wsg_ctx* const* ctxs, int nctx)
 {
-    const char* e = std::getenv("WSG_HOST_MULTI_SHARE");
+    const char* e = wsg::envp("WSG_HOST_MULTI_SHARE");
     const bool share = e && *e == '1';
     std::vector<wsg_ctx*> v;
     std::vector<int> seen;
@@ -276,6 +277,7 @@ int wsg_mgpu_unique_id(uint8_t* id)
 {
     if (!id)
         return WSG_EINVAL;
+    wsg::hip_init_once();
     const Rccl* r = rccl();
     if (!r)
         return WSG_EHIP;
@@ -350,6 +352,7 @@ int wsg_mgpu_create(const int* devices, int ndev, wsg_mgpu** out)
 {
     if (!out || !devices || ndev <= 0)
         return WSG_EINVAL;
+    wsg::hip_init_once();
     *out = nullptr;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess)
@@ -380,6 +383,7 @@ int wsg_mgpu_create_rank(int device, const uint8_t* id, int rank, int world, wsg
 {
     if (!out || !id || world <= 0 || rank < 0 || rank >= world)
         return WSG_EINVAL;
+    wsg::hip_init_once();
     *out = nullptr;
     const Rccl* r = rccl();
     if (!r)
