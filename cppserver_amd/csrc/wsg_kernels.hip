@@ -2441,6 +2441,167 @@ hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64
     return hipGetLastError();
 }
 
+// ---- fan-out, grid path (many messages in one call) ------------------------
+// The same chunk formula as the period path, laid out as the plain fill the
+// write stream runs fastest as (tools/membench.hip: one 16-B store per lane
+// and a grid over every chunk, 98 us for 657 MB against 106-117 us for the
+// period kernel's 1 KiB rows per wave per pass): a small first kernel
+// writes every message's G chunk templates (T, MA, MB, the key rotations,
+// the frame of the group) into a table, and the second gives every chunk of
+// every message one lane — its group from one float multiply, its template
+// and its one or two keys from L2, one nontemporal store.
+struct FanEntry {
+    v4u t, ma, mb;
+    uint32_t w[4];   // w[0] = frame of the group (qa) | sa << 8 | sbr << 16 | has_b << 24
+};
+static_assert(sizeof(FanEntry) == 64, "fan-out table entry");
+
+template <int P>
+__global__ __launch_bounds__(256) void k_fanout_tables(const uint8_t* __restrict__ payload0, uint64_t len,
+                                                       uint8_t opcode, uint32_t mask, uint64_t fsize, uint32_t G,
+                                                       const FanMsgs msgs, v4u hp0, FanEntry* __restrict__ tab)
+{
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= G)
+        return;
+    const uint8_t* __restrict__ payload = payload0 + msgs.src[blockIdx.y];
+    FanGeom f;   // as k_fanout_period
+    f.g = send_geom(opcode, mask != 0, len, 0);
+    f.data0 = f.g.hdr + f.g.prefix;
+    f.kpos = f.g.hdr - (mask ? 4u : 0u);
+    f.mask = mask != 0;
+    f.hp0 = hp0;
+    const uint64_t o = uint64_t(j) * CHUNK;
+    uint32_t qa = 0;
+#pragma unroll
+    for (int q = 1; q < P; ++q)
+        qa += o >= uint64_t(q) * fsize ? 1u : 0u;
+    const uint64_t r = o - uint64_t(qa) * fsize;
+    v4u t, ma, mb = {0, 0, 0, 0};
+    fan_tm(payload, len, f, fsize, r, t, ma);
+    const uint64_t split = fsize - r;
+    uint32_t hb = 0;
+    if (split < CHUNK) {
+        v4u t0, m0v;
+        fan_tm(payload, len, f, fsize, 0, t0, m0v);
+        t |= shl_bytes(t0, split);
+        mb = shl_bytes(m0v, split);
+        hb = 1;
+    }
+    const uint32_t pa = uint32_t(r - f.g.hdr), pb = uint32_t(0u - uint32_t(split) - f.g.hdr);
+    FanEntry e;
+    e.t = t;
+    e.ma = ma;
+    e.mb = mb;
+    e.w[0] = qa | ((8u * (pa & 3u)) << 8) | ((8u * (pb & 3u)) << 16) | (hb << 24);
+    e.w[1] = e.w[2] = e.w[3] = 0;
+    tab[size_t(blockIdx.y) * G + j] = e;
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void k_fanout_grid(const uint32_t* __restrict__ keys, uint32_t k, uint32_t G,
+                                                     float inv_g, uint32_t chunks, uint64_t total,
+                                                     uint8_t* __restrict__ wire0, const FanMsgs msgs,
+                                                     const FanEntry* __restrict__ tab)
+{
+    const uint32_t c = blockIdx.x * 256 + threadIdx.x;   // chunk of message blockIdx.y (host: chunks < 2^24)
+    if (c >= chunks)
+        return;
+    int32_t g = int32_t(float(c) * inv_g);               // its group, exact after one correction
+    int32_t j = int32_t(c) - g * int32_t(G);
+    if (j < 0) {
+        --g;
+        j += int32_t(G);
+    } else if (j >= int32_t(G)) {
+        ++g;
+        j -= int32_t(G);
+    }
+    const FanEntry* __restrict__ e = tab + size_t(blockIdx.y) * G + uint32_t(j);
+    const uint32_t w = e->w[0];
+    const uint32_t ia = uint32_t(g) * P + (w & 0xFFu);
+    const bool hb = (w >> 24) != 0;
+    const uint32_t ka = ia < k ? keys[ia] : 0u;
+    const uint32_t kb = (hb && ia + 1 < k) ? keys[ia + 1] : 0u;
+    const uint32_t ra = __builtin_amdgcn_alignbit(ka, ka, (w >> 8) & 0xFFu);
+    const uint32_t rb = __builtin_amdgcn_alignbit(kb, kb, (w >> 16) & 0xFFu);
+    const v4u out = e->t ^ (e->ma & v4u{ra, ra, ra, ra}) ^ (e->mb & v4u{rb, rb, rb, rb});
+    uint8_t* __restrict__ wire = wire0 + msgs.dst[blockIdx.y];
+    if (c + 1 < chunks || (total & (CHUNK - 1)) == 0) {
+        st16nt(wire + uint64_t(c) * CHUNK, out);
+    } else {
+#pragma unroll 1
+        for (uint32_t b = 0; b < uint32_t(total & (CHUNK - 1)); ++b)
+            wire[uint64_t(c) * CHUNK + b] = uint8_t(lane_byte(out, b));
+    }
+}
+
+// Grid path for nmsgs messages of one geometry when the frame size allows
+// the period formula and each message's chunks fit 2^24; `table` holds at
+// least fanout_grid_table_bytes(...) bytes.  false: not taken.
+bool fanout_grid_shape(uint64_t fsize, uint32_t k, uint32_t& P, uint32_t& G)
+{
+    if (fsize % 4 != 0)
+        return false;
+    uint64_t g16 = 16;
+    while (fsize % g16)
+        g16 >>= 1;
+    P = uint32_t(16 / g16);
+    const uint64_t g = uint64_t(P) * fsize / CHUNK;
+    const uint64_t chunks = (fsize * k + CHUNK - 1) / CHUNK;
+    if (g < 1 || g > (1u << 20) || chunks >= (uint64_t(1) << 24) || uint64_t(k) * P >= (uint64_t(1) << 31))
+        return false;
+    G = uint32_t(g);
+    return true;
+}
+
+uint64_t fanout_grid_table_bytes(uint64_t fsize, uint32_t k, uint32_t nmsgs)
+{
+    uint32_t P, G;
+    if (!fanout_grid_shape(fsize, k, P, G))
+        return 0;
+    return uint64_t(nmsgs) * G * sizeof(FanEntry);
+}
+
+bool launch_fanout_grid(hipStream_t s, const uint8_t* payload, uint64_t len, const uint32_t* keys, uint32_t k,
+                        uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire, const FanMsgs& msgs,
+                        uint32_t nmsgs, void* table, uint64_t table_bytes, hipError_t* err)
+{
+    uint32_t P, G;
+    if (nmsgs == 0 || nmsgs > uint32_t(FAN_MSGS) || !fanout_grid_shape(fsize, k, P, G) ||
+        table_bytes < uint64_t(nmsgs) * G * sizeof(FanEntry) || !table)
+        return false;
+    for (uint32_t y = 0; y < nmsgs; ++y)
+        if (((reinterpret_cast<uintptr_t>(wire) + msgs.dst[y]) & (CHUNK - 1)) != 0)
+            return false;   // (16-B stores at each message's start)
+    const uint64_t total = fsize * k;
+    const uint32_t chunks = uint32_t((total + CHUNK - 1) / CHUNK);
+    const SendGeom sg = send_geom(opcode, mask != 0, len, 0);
+    const uint32_t kpos = sg.hdr - (mask ? 4u : 0u);
+    uint32_t hw[4] = {0, 0, 0, 0};
+    for (uint32_t r = 0; r < kpos; ++r)
+        hw[r / 4] |= uint32_t(header_byte(opcode, mask != 0, sg.body, 0, r)) << (8 * (r % 4));
+    const v4u hp0 = v4u{hw[0], hw[1], hw[2], hw[3]};
+    FanEntry* tab = static_cast<FanEntry*>(table);
+    const dim3 tg((G + 255) / 256, nmsgs), sg2((chunks + 255) / 256, nmsgs);
+    const float inv_g = 1.0f / float(G);
+    switch (P) {
+    case 1:
+        k_fanout_tables<1><<<tg, 256, 0, s>>>(payload, len, opcode, mask, fsize, G, msgs, hp0, tab);
+        k_fanout_grid<1><<<sg2, 256, 0, s>>>(keys, k, G, inv_g, chunks, total, wire, msgs, tab);
+        break;
+    case 2:
+        k_fanout_tables<2><<<tg, 256, 0, s>>>(payload, len, opcode, mask, fsize, G, msgs, hp0, tab);
+        k_fanout_grid<2><<<sg2, 256, 0, s>>>(keys, k, G, inv_g, chunks, total, wire, msgs, tab);
+        break;
+    default:
+        k_fanout_tables<4><<<tg, 256, 0, s>>>(payload, len, opcode, mask, fsize, G, msgs, hp0, tab);
+        k_fanout_grid<4><<<sg2, 256, 0, s>>>(keys, k, G, inv_g, chunks, total, wire, msgs, tab);
+        break;
+    }
+    *err = hipGetLastError();
+    return true;
+}
+
 // Period path (k_fanout_period) when the frame size allows it; returns false
 // to leave the batch to k_fanout_flat.  Wave count W = Q * s with W * 64 a
 // multiple of G (Q = G / gcd(G, 64)), about `waves` of them, and few enough

@@ -452,6 +452,67 @@ def test_fanout_many_vs_oracle(codec, case):
         assert int(off[m]) == int(off[m - 1]) + k * frame_size(int(ops[-1]), mask, int(lens[-1]))
 
 
+@pytest.mark.parametrize("length,k,opcode", [
+    (4092, 7, 0x82),     # F = 4100: P = 4, G = 1025, the last chunk partial (total % 16 = 12)
+    (4096, 3, 0x82),     # F = 4104: P = 2 (C4's geometry), total % 16 = 8
+    (4088, 5, 0x81),     # F = 4096: P = 1
+    (122, 1000, 0x82),   # F = 128: G = 8 (below the period kernel's 64)
+    (58, 33, 0x82),      # F = 64: G = 4
+    (8190, 130, 0x89),   # ping with the status prefix: F = 8200, P = 2
+    (65538, 40, 0x82),   # 8-byte length form: F = 65552
+])
+def test_fanout_grid_path(length, k, opcode):
+    """With $WSG_FAN_GRID=2 (an A/B knob, off by default), calls of several
+    messages of one geometry take the grid path (k_fanout_tables +
+    k_fanout_grid: one lane per chunk): every message's
+    frames equal oracle.fanout_encode's, as the period path's
+    ($WSG_FAN_GRID=0) do, masked and unmasked."""
+    import os
+
+    rng = np.random.default_rng(length * 31 + k)
+    m = 3
+    keys = rng.integers(0, 2**32, k, dtype=np.uint64).astype(np.uint32)
+    lens = np.full(m, length)
+    ops = np.full(m, opcode)
+    src = np.zeros(m, np.uint64)
+    src[1:] = np.cumsum(lens[:-1] + 5)            # unaligned message starts
+    arena = wl.random_bytes(rng, int(src[-1] + lens[-1] + 16))
+    old = os.environ.get("WSG_FAN_GRID")
+    try:
+        os.environ["WSG_FAN_GRID"] = "0"
+        period = ca.Codec(0)
+    finally:
+        if old is None:
+            os.environ.pop("WSG_FAN_GRID", None)
+        else:
+            os.environ["WSG_FAN_GRID"] = old
+    try:
+        os.environ["WSG_FAN_GRID"] = "2"
+        grid = ca.Codec(0)
+    finally:
+        if old is None:
+            os.environ.pop("WSG_FAN_GRID", None)
+        else:
+            os.environ["WSG_FAN_GRID"] = old
+    try:
+        for mask in (True, False):
+            outs = []
+            for c in (grid, period):
+                wire_t, off = c.fanout_many(dev(arena), src, lens, ops, dev(keys.view(np.int32)), mask=mask)
+                c.sync()
+                outs.append((wire_t.cpu().numpy(), off))
+            (got, off), (per, off_p) = outs
+            assert np.array_equal(off, off_p)
+            for i in range(m):   # (the padding between messages is not written by either path)
+                ref = oracle.fanout_encode(arena[int(src[i]): int(src[i]) + length], keys, opcode, mask)
+                a = int(off[i])
+                assert np.array_equal(got[a: a + len(ref)], ref), (i, mask)
+                assert np.array_equal(per[a: a + len(ref)], ref), (i, mask)
+    finally:
+        grid.close()
+        period.close()
+
+
 def test_fanout_many_capacity(codec):
     keys = torch.zeros(4, dtype=torch.int32, device="cuda")
     with pytest.raises(ca.WSGError) as e:
