@@ -502,13 +502,15 @@ def pcie_inclusive(w, reps=3):
     return res
 
 
-def _run_leg(cmd, timeout):
+def _run_leg(cmd, timeout, env=None):
     """A host-side leg's child process; a time-out is reported in the line
-    (returncode 124) rather than ending the bench."""
+    (returncode 124) rather than ending the bench.  env: variables added to
+    this process's environment for the child."""
     import subprocess
 
     try:
-        return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+        return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout,
+                              env=dict(os.environ, **env) if env else None)
     except subprocess.TimeoutExpired:
         return subprocess.CompletedProcess(cmd, 124, "", "no result within %d s" % timeout)
 
@@ -612,10 +614,16 @@ def echo_c1_leg(seconds=3.0, timeout=120):
     tcp = os.path.join(ROOT, "tools", "_build", "bench_echo_tcp")
     if os.path.exists(tcp):
         tr = {}
-        for leg, a in (("gpu_1c_1t", ["gpu", "1", "1"]), ("gpu_100c_4t", ["gpu", "100", "4"]),
-                       ("gpu_tick_100c_4t", ["gpu_tick", "100", "4"]),
-                       ("cpu_ref_1c_1t", ["cpu_ref", "1", "1"]), ("cpu_ref_100c_4t", ["cpu_ref", "100", "4"])):
-            r = _run_leg([tcp] + a + ["1000", "32", str(seconds)], timeout)
+        # gpu_100c_4t_hwq8: the same with one hardware queue per IO thread
+        # (GPU_MAX_HW_QUEUES=8 for the 4 server + 4 client threads; the
+        # library then gives each thread's context a lane): a runtime setting
+        # of the deployment, reported beside the default one
+        for leg, a, env in (("gpu_1c_1t", ["gpu", "1", "1"], None), ("gpu_100c_4t", ["gpu", "100", "4"], None),
+                            ("gpu_100c_4t_hwq8", ["gpu", "100", "4"], {"GPU_MAX_HW_QUEUES": "8"}),
+                            ("gpu_tick_100c_4t", ["gpu_tick", "100", "4"], None),
+                            ("cpu_ref_1c_1t", ["cpu_ref", "1", "1"], None),
+                            ("cpu_ref_100c_4t", ["cpu_ref", "100", "4"], None)):
+            r = _run_leg([tcp] + a + ["1000", "32", str(seconds)], timeout, env)
             if r.returncode != 0:
                 tr[leg] = {"error": (r.stderr or r.stdout).strip()[-300:]}
                 continue

@@ -720,6 +720,16 @@ int wsg_create(int device, wsg_ctx** out)
         c->lane_max = std::strtoull(e, nullptr, 10);
     if (const char* e = wsg::envp("WSG_LANE_PROFILE"))
         c->lane_profile = *e == '1';
+    // default: one lane per hardware queue the runtime gives a priority
+    // ($GPU_MAX_HW_QUEUES, 4 unless set): past that, lanes share queues and
+    // each launch of one waits behind another's resident kernel (TCP echo,
+    // 4+4 threads: 26 M msg/s with 8 lanes on 4 queues, 55 M on 8 queues,
+    // profiles/r4/lane_hwq_ab.log)
+    if (const char* e = wsg::envp("GPU_MAX_HW_QUEUES")) {
+        const long v = std::atol(e);
+        if (v >= 1 && v <= 64)
+            c->lane_cap = int(v);
+    }
     if (const char* e = wsg::envp("WSG_LANE_CAP")) {
         const long v = std::atol(e);
         if (v >= 1 && v <= (1l << 20))
