@@ -343,8 +343,8 @@ int wsg_timing_minmax(wsg_ctx* ctx, double* min_ms, double* max_ms);
  * $WSG_LANE_IDLE_US (default 2000) without a request and after every
  * $WSG_LANE_REQS-th request (default 256: a running kernel holds up calls
  * that wait for the device to drain), and the next call launches it again.
- * At most $WSG_LANE_CAP contexts of a process (default 4) hold a lane; the
- * others take the launch paths.
+ * At most $WSG_LANE_CAP contexts of a process (default: $GPU_MAX_HW_QUEUES,
+ * else 4) hold a lane; the others take the launch paths.
  * Requests it answered, its launches, and whether it runs now (1), has left
  * (0) or stopped answering (-1: the launch paths from then on).            */
 int wsg_lane_stats(wsg_ctx* ctx, uint64_t* requests, uint64_t* launches, int* running);
