@@ -372,8 +372,8 @@ class Codec:
         return lo.value, hi.value
 
     def lane_stats(self):
-        """(requests, launches, running) of the context's host lane
-        (wsg_lane_stats: small page-locked host batches)."""
+        """(requests this context put on the lane, launches of the device's
+        lane, running: 1 / 0 / -1 given up) — wsg_lane_stats."""
         r, l, on = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
         _check(self._L.wsg_lane_stats(self._ctx, ctypes.byref(r), ctypes.byref(l), ctypes.byref(on)),
                "wsg_lane_stats")

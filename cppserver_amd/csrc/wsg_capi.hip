@@ -15,6 +15,7 @@
 #include <map>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 // Encode scratch (scan partials, piece starts, piece -> frame map); the ctx
@@ -40,12 +41,12 @@ struct wsg_ctx {
     // round 3); at or under a grid's worth of pieces the two are the same
     int enc_blocks_per_cu = 32768;
     uint64_t enc_launch_pieces = 0;   // k_encode_mask: pieces per launch (0: all in one)
-    uint64_t xor_direct_max = 64 << 10;   // per-call XOR: kernel on the pinned stage up to this size (A/B: $WSG_XOR_DIRECT_MAX)
+    uint64_t xor_direct_max = 64 << 10;   // per-call XOR off the lane: kernel on the pinned stage up to this size
+    uint64_t seg_bytes = 32ull << 20;     // staged host pipelines: segment of about this many wire bytes ($WSG_STAGE_MB)
     // host batches up to this many wire bytes whose buffers are page-locked:
     // the kernels read and write them in place (one launch sequence and one
     // synchronize, no staging copies); $WSG_HOST_DIRECT_MAX
     uint64_t host_direct_max = 4 << 20;   // 1-4 MB batches 1.6-2x faster direct, 16 MB even (profiles/r3/host_direct_sizes.log)
-    int dec_tiles_per_block = 0;   // 0: grid from dec_blocks_per_cu alone; k: ceil(tiles / k) blocks (A/B)
     bool check = false;            // $WSG_CHECK=1: operand ranges validated before every device launch (debug)
     int dec_blocks_per_cu = 4096;  // k_decode grid cap: one 16 KiB tile per block up to 16 GiB of wire (tools/tune.py, round 2: C2 84.3 vs 85.1 us at 48 blocks/CU, 88.1 at two tiles per block; C3 ragged 0.685 vs 0.705 ms at 256, 0.783 at 48)
     int fan_waves_per_cu = 6;    // fan-out period path: waves per CU (tools/c4_ab.py, graph-replayed C4: 6 -> 8.10 us, 4 -> 8.16, 8 -> 8.32)
@@ -112,36 +113,18 @@ struct wsg_ctx {
     Slot slots[kSlots];
     // role streams of the host pipelines: every H2D copy on one stream, every
     // kernel on another, every D2H copy on a third, so the two copy directions
-    // run concurrently while kernels run between them ($WSG_PIPE=slots: one
-    // stream per slot instead, the earlier design, kept for A/B runs)
+    // run concurrently while kernels run between them
     hipStream_t s_h2d = nullptr, s_kern = nullptr, s_d2h = nullptr;
     // the host lane (wsg_internal.h): page-locked host batches of at most
-    // lane_max wire bytes go to a resident kernel of lane_wgs workgroups
-    // through a doorbell instead of a launch + synchronize ($WSG_LANE_MAX,
-    // 0 = never; $WSG_LANE_WGS)
-    struct Lane {
-        wsg::LaneBell* bell = nullptr;   // page-locked, coherent
-        hipStream_t stream = nullptr;
-        bool running = false;            // launched, not yet seen leaving
-        bool broken = false;             // did not answer: the launch paths from now on
-        bool declined = false;           // the process already holds lane_cap lanes: the launch paths
-        uint64_t seq = 0;
-        uint64_t launches = 0;           // kernel launches of the lane (wsg_lane_stats)
-        uint32_t gen = 0;                // the running launch's number (exited[] holds it when it leaves)
-    } lane;
+    // lane_max wire bytes (and per-call XORs of at most that many bytes) go to
+    // the device's resident lane, shared by every context of the process,
+    // through its mailboxes instead of a launch + synchronize ($WSG_LANE_MAX,
+    // 0 = never)
+    struct LaneServer* lane = nullptr;   // the device's (made on first use)
     uint64_t lane_max = 64 << 10;
-    uint32_t lane_wgs = 8;          // workgroups (CUs) sharing a request's reads and writes
-    int lane_cap = 4;               // this context takes a lane only while the process holds fewer ($WSG_LANE_CAP)
-    bool tables_in_place = true;    // the direct paths use tables in wsg_host_alloc blocks in place ($WSG_TABLES_IN_PLACE, A/B)
-    uint32_t lane_idle_us = 2000;   // the lane leaves after this long without a request
-    uint32_t lane_reqs = 256;       // ... and after every lane_reqs-th request ($WSG_LANE_REQS)
-    // $WSG_LANE_PROFILE=1: where a lane request's time goes (host: before the
-    // ring, the wait, after the answer; lane: pick-up to staged, to parsed /
-    // heads built, to done, the release fence), printed when the lane stops
-    bool lane_profile = false;
-    double lane_prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t lane_prof_n = 0;
-    int wall_khz = 100000;          // constant clock of the lane's idle limit
+    uint32_t lane_groups = wsg::LANE_GROUPS_MAX;   // most frame groups of one request ($WSG_LANE_GROUPS)
+    uint64_t lane_requests = 0;          // requests this context put on the lane (wsg_lane_stats)
+    bool dead = false;                   // a lane request neither answered nor drained: buffers may still be written
     // timing of the dominant kernel
     struct EvPair {
         hipEvent_t a, b;
@@ -305,17 +288,10 @@ bool in_alloc(const void* p, uint64_t bytes)
 namespace {
 
 // Page-locked host memory the kernels read and write in place (the session
-// batches' buffers, the direct paths' tables): coherent (fine-grained)
-// when $WSG_HOST_COHERENT=1, else the runtime's default (A/B: the lane's
-// PCIe reads of it, tools/lane_ab.py).
-unsigned host_alloc_flags()
-{
-    static const unsigned f = [] {
-        const char* e = wsg::envp("WSG_HOST_COHERENT");
-        return (e && *e == '1') ? unsigned(hipHostMallocCoherent | hipHostMallocMapped) : unsigned(hipHostMallocDefault);
-    }();
-    return f;
-}
+// batches' buffers, the direct paths' tables): the runtime's default
+// (mapped at the same address on the device).  The lane's system-scope
+// acquire / release fences keep its reads and writes of it coherent.
+unsigned host_alloc_flags() { return unsigned(hipHostMallocDefault); }
 
 // The blocks wsg_host_alloc made (page-locked, mapped at the same address on
 // the device): a host batch in one of them (the session batches' buffers
@@ -379,237 +355,309 @@ bool in_host_block(const void* p, uint64_t bytes = 1)
 
 // ---- the host lane --------------------------------------------------------
 
+// One lane per device, shared by every context of the process on it
+// (wsg_internal.h): its mailboxes, its stream and the launches of its
+// resident kernel.  Servers are made on first use and live as long as the
+// process (the at-exit handler stops their kernels).
+struct LaneServer {
+    int device = 0;
+    wsg::LaneBell* bell = nullptr;   // page-locked, coherent, mapped
+    hipStream_t stream = nullptr;
+    uint32_t W = 8;                  // workgroups ($WSG_LANE_WGS)
+    uint64_t idle_ticks = 0, yield_ticks = 0, delay_ticks = 0;
+    int timeout_ms = 5000;           // a request unanswered this long: the lane is given up ($WSG_LANE_TIMEOUT_MS)
+    int drain_ms = 2000;             // ... and waited for this long to leave ($WSG_LANE_DRAIN_MS)
+    std::mutex launch_lock;
+    std::atomic<uint32_t> gen{0};        // the last launch's generation (0: none yet)
+    std::atomic<bool> broken{false};     // given up: no more launches, every caller takes the launch paths
+    std::atomic<uint64_t> tickets{0};    // next ticket
+    std::atomic<int> inflight{0};        // requests posted and not yet answered
+    std::atomic<uint64_t> launches{0};
+    // per mailbox slot: the last ticket + 1 whose caller has read its answer
+    // (a slot is reused only after that: its previous task done and read)
+    std::atomic<uint64_t> released[wsg::LANE_WGS_MAX * wsg::LANE_RING];
+};
+
 namespace {
 
-// Every context with a lane, so that a process ending without wsg_destroy
-// still stops them (the lanes also leave on their own after lane_idle_us).
-std::mutex& lane_registry_lock()
+std::mutex& lane_servers_lock()
 {
     static std::mutex* m = new std::mutex;   // leaked: used at exit
     return *m;
 }
-std::vector<wsg_ctx*>& lane_registry()
+std::map<int, LaneServer*>& lane_servers()
 {
-    static auto* v = new std::vector<wsg_ctx*>;
+    static auto* v = new std::map<int, LaneServer*>;
     return *v;
 }
 
-void lane_report(wsg_ctx* c)
+// Wait (at most ms) until every launch on the lane's stream has ended.
+bool lane_drained(LaneServer* s, int ms)
 {
-    if (!c->lane_profile || !c->lane_prof_n)
-        return;
-    const double n = double(c->lane_prof_n);
-    const double* p = c->lane_prof;
-    std::fprintf(stderr,
-                 "WSG_LANE_PROFILE {\"requests\": %llu, \"host_prep_us\": %.2f, \"host_wait_us\": %.2f, "
-                 "\"host_post_us\": %.2f, \"lane_stage_us\": %.2f, \"lane_frames_us\": %.2f, \"lane_rest_us\": %.2f, "
-                 "\"lane_fence_us\": %.2f, \"bell_us\": %.2f, \"launches\": %llu}\n",
-                 (unsigned long long)c->lane_prof_n, p[0] / n, p[1] / n, p[2] / n, p[3] / n, p[4] / n, p[5] / n, p[6] / n,
-                 p[7] / n, (unsigned long long)c->lane.launches);
-    c->lane_prof_n = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipStreamQuery(s->stream);
+        if (q == hipSuccess)
+            return true;
+        if (q != hipErrorNotReady) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(ms))
+            return false;
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
 }
 
-// Ask the lane to leave and wait until it has (its kernel has ended; a
-// launch that ended after its last request may still be finishing).
-void lane_stop(wsg_ctx* c)
-{
-    if (!c->lane.bell || !c->lane.launches)
-        return;
-    (void)hipSetDevice(c->device);
-    __atomic_store_n(&c->lane.bell->stop, 1u, __ATOMIC_RELEASE);
-    (void)hipStreamSynchronize(c->lane.stream);
-    c->lane.running = false;
-}
-
+// Every lane told to leave at process exit (a lane also leaves on its own
+// after its idle limit); a lane already given up is not waited for again.
 void lanes_at_exit()
 {
-    std::lock_guard<std::mutex> g(lane_registry_lock());
-    for (wsg_ctx* c : lane_registry()) {
-        lane_stop(c);
-        lane_report(c);
+    std::lock_guard<std::mutex> g(lane_servers_lock());
+    for (auto& kv : lane_servers()) {
+        LaneServer* s = kv.second;
+        if (s->broken.load() || s->gen.load() == 0)
+            continue;
+        __atomic_store_n(&s->bell->ctl.stop, 1u, __ATOMIC_RELEASE);
+        (void)lane_drained(s, 1000);
     }
 }
 
-// Launch the lane if it is not running (first use, or it left idle).
-int lane_start(wsg_ctx* c)
+// The device's lane, made on first use (nullptr: it cannot be made).
+LaneServer* lane_server(int device)
 {
-    if (!c->lane.bell) {
-        void* p = nullptr;
-        if (hipHostMalloc(&p, sizeof(wsg::LaneBell), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-            return WSG_ENOMEM;
-        std::memset(p, 0, sizeof(wsg::LaneBell));
-        c->lane.bell = static_cast<wsg::LaneBell*>(p);
-        // A running lane holds the hardware queue its stream is on: every
-        // packet queued behind it waits until the launch ends.  The runtime
-        // keeps streams of each priority on their own queues, so the lanes
-        // go on high-priority streams (ahead of nothing but other lanes) and
-        // the contexts' ordinary streams never queue behind one
-        // ($WSG_LANE_PRIORITY=0: the default priority, A/B)
-        int lo = 0, hi = 0;
-        const char* pe = wsg::envp("WSG_LANE_PRIORITY");
-        const bool made = (!pe || *pe != '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess
-                              ? hipStreamCreateWithPriority(&c->lane.stream, hipStreamNonBlocking, hi) == hipSuccess
-                              : hipStreamCreateWithFlags(&c->lane.stream, hipStreamNonBlocking) == hipSuccess;
-        if (!made) {   // (never a launch on the null stream: the doorbell goes, the next call tries again)
-            c->lane.stream = nullptr;
+    std::lock_guard<std::mutex> g(lane_servers_lock());
+    auto& m = lane_servers();
+    auto it = m.find(device);
+    if (it != m.end())
+        return it->second;
+    auto* s = new (std::nothrow) LaneServer;
+    if (!s)
+        return nullptr;
+    s->device = device;
+    for (auto& r : s->released)
+        r.store(0, std::memory_order_relaxed);
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0)
+        khz = 100000;   // 100 MHz, the gfx9 constant clock
+    long idle_us = 2000, yield_us = 2000, delay_us = 0;
+    {
+        std::lock_guard<std::recursive_mutex> eg(wsg::env_mutex());
+        if (const char* e = wsg::envp("WSG_LANE_WGS")) {
+            const long v = std::atol(e);
+            if (v >= 1 && v <= long(wsg::LANE_WGS_MAX))
+                s->W = uint32_t(v);
+        }
+        if (const char* e = wsg::envp("WSG_LANE_IDLE_US"))
+            idle_us = std::max(1l, std::min(1000000l, std::atol(e)));
+        if (const char* e = wsg::envp("WSG_LANE_YIELD_US"))
+            yield_us = std::max(1l, std::min(1000000l, std::atol(e)));
+        if (const char* e = wsg::envp("WSG_LANE_TIMEOUT_MS"))
+            s->timeout_ms = int(std::max(1l, std::min(600000l, std::atol(e))));
+        if (const char* e = wsg::envp("WSG_LANE_DRAIN_MS"))
+            s->drain_ms = int(std::max(1l, std::min(600000l, std::atol(e))));
+        if (const char* e = wsg::envp("WSG_TEST_LANE_DELAY_US"))   // test hook: the kernel starts late
+            delay_us = std::max(0l, std::min(10000000l, std::atol(e)));
+    }
+    s->idle_ticks = uint64_t(idle_us) * uint64_t(khz) / 1000u;
+    s->yield_ticks = uint64_t(yield_us) * uint64_t(khz) / 1000u;
+    s->delay_ticks = uint64_t(delay_us) * uint64_t(khz) / 1000u;
+    void* p = nullptr;
+    int dev0 = 0;
+    (void)hipGetDevice(&dev0);
+    // A running lane holds the hardware queue its stream is on: every packet
+    // queued behind it waits until the launch ends.  The runtime keeps streams
+    // of each priority on their own queues, so the lane goes on a
+    // high-priority stream (ahead of nothing but itself) and the contexts'
+    // ordinary streams never queue behind it.
+    int lo = 0, hi = 0;
+    const bool ok = hipSetDevice(device) == hipSuccess &&
+                    hipHostMalloc(&p, sizeof(wsg::LaneBell), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+                    hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+                    hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, hi) == hipSuccess;
+    (void)hipSetDevice(dev0);
+    if (!ok) {
+        if (p)
             (void)hipHostFree(p);
-            c->lane.bell = nullptr;
-            return WSG_EHIP;
+        delete s;
+        return nullptr;
+    }
+    std::memset(p, 0, sizeof(wsg::LaneBell));
+    s->bell = static_cast<wsg::LaneBell*>(p);
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit(lanes_at_exit); });
+    m[device] = s;
+    return s;
+}
+
+// Give the lane up (a request went unanswered): no launch from now on, and
+// every workgroup leaves at its next check without taking another task.
+void lane_give_up(LaneServer* s)
+{
+    std::lock_guard<std::mutex> g(s->launch_lock);
+    s->broken.store(true);
+    __atomic_store_n(&s->bell->ctl.stop, 1u, __ATOMIC_RELEASE);
+}
+
+// Launch the next generation if generation `seen` is the last one (none yet,
+// or it announced its end): queued behind it on the lane's stream, it starts
+// once every workgroup of the old one has left, each mailbox where it was.
+void lane_relaunch(LaneServer* s, uint32_t seen)
+{
+    std::lock_guard<std::mutex> g(s->launch_lock);
+    if (s->broken.load() || s->gen.load() != seen)
+        return;
+    uint32_t next = seen + 1;
+    if (next == 0)
+        next = 1;
+    if (wsg::launch_lane(s->stream, s->bell, s->W, s->idle_ticks, s->yield_ticks, next, s->delay_ticks) != hipSuccess) {
+        (void)hipGetLastError();
+        s->broken.store(true);
+        __atomic_store_n(&s->bell->ctl.stop, 1u, __ATOMIC_RELEASE);
+        return;
+    }
+    s->launches.fetch_add(1);
+    s->gen.store(next);
+}
+
+// A launch running (or queued) that has not announced its end; else launch.
+void lane_ensure_running(LaneServer* s)
+{
+    const uint32_t g = s->gen.load(std::memory_order_acquire);
+    if (g == 0 || __atomic_load_n(&s->bell->ctl.closing, __ATOMIC_ACQUIRE) == g)
+        lane_relaunch(s, g);
+}
+
+// The lane for this context's request, or nullptr (lane off for the context,
+// the lane given up, or it cannot be made).
+LaneServer* lane_for(wsg_ctx* c)
+{
+    if (!c->lane_max)
+        return nullptr;
+    if (!c->lane) {
+        c->lane = lane_server(c->device);
+        if (!c->lane) {
+            c->lane_max = 0;
+            return nullptr;
         }
-        static std::once_flag once;
-        std::call_once(once, [] { std::atexit(lanes_at_exit); });
-        std::lock_guard<std::mutex> g(lane_registry_lock());
-        lane_registry().push_back(c);
     }
-    if (c->lane.running)
-        return WSG_OK;
-    wsg::LaneBell* b = c->lane.bell;
-    b->stop = 0;
-    // (queued behind the previous launch on the lane's stream when that one
-    // is still ending: it starts from each workgroup's `done`)
-    const uint64_t idle = uint64_t(c->lane_idle_us) * uint64_t(c->wall_khz) / 1000u;
-    if (++c->lane.gen == 0)
-        ++c->lane.gen;
-    if (wsg::launch_lane(c->lane.stream, b, c->lane_wgs, idle, c->lane.gen, c->lane_reqs) != hipSuccess)
-        return WSG_EHIP;
-    c->lane.running = true;
-    ++c->lane.launches;
-    return WSG_OK;
+    return c->lane->broken.load(std::memory_order_relaxed) ? nullptr : c->lane;
 }
 
-// Frames per group for a request of n frames: the workgroups share the
-// frames evenly, a group at most LANE_THREADS frames, and no workgroup takes
-// more than LANE_GROUPS_PER_WG groups (n <= lane_max_frames).
-uint32_t lane_max_frames(const wsg_ctx* c)
+// Frame groups for a request of n frames: as many as the lane has idle
+// workgroups (W shared among the requests in flight), at most the context's
+// lane_groups, at least one per LANE_THREADS frames.  Returns the frames per
+// group; *groups = ceil(n / that).
+uint32_t lane_split(const wsg_ctx* c, const LaneServer* s, uint32_t n, uint32_t* groups)
 {
-    return std::min<uint32_t>(wsg::LANE_GROUPS_MAX, c->lane_wgs * wsg::LANE_GROUPS_PER_WG) * wsg::LANE_THREADS;
-}
-uint32_t lane_group_size(const wsg_ctx* c, uint32_t n)
-{
-    uint32_t G = (n + c->lane_wgs - 1) / c->lane_wgs;
-    G = std::max<uint32_t>(G, (n + c->lane_wgs * wsg::LANE_GROUPS_PER_WG - 1) / (c->lane_wgs * wsg::LANE_GROUPS_PER_WG));
-    G = std::max<uint32_t>(G, (n + wsg::LANE_GROUPS_MAX - 1) / wsg::LANE_GROUPS_MAX);
-    return std::max<uint32_t>(1, std::min<uint32_t>(G, wsg::LANE_THREADS));
+    const uint32_t busy = uint32_t(std::max(0, s->inflight.load(std::memory_order_relaxed))) + 1;
+    uint32_t g = std::max<uint32_t>(1, s->W / busy);
+    g = std::min(g, c->lane_groups);
+    g = std::max(g, (n + wsg::LANE_THREADS - 1) / wsg::LANE_THREADS);
+    g = std::max<uint32_t>(1, std::min(g, n));
+    const uint32_t per = (n + g - 1) / g;
+    *groups = (n + per - 1) / per;
+    return per;
 }
 
-// One request on the lane (the group ranges already in bell->grp); returns
-// when every workgroup has answered.  WSG_EHIP when the lane does not answer
-// within seconds (it is then not used again).
-int lane_call(wsg_ctx* c, uint32_t op, uint32_t n, uint32_t G, const uint64_t (&a)[6])
+// Requests of at most this many frames fit the lane (groups of at most
+// LANE_THREADS frames, at most LANE_GROUPS_MAX groups).
+constexpr uint32_t kLaneMaxFrames = wsg::LANE_GROUPS_MAX * wsg::LANE_THREADS;
+
+enum LaneResult { LANE_DONE = 0, LANE_FALLBACK = 1, LANE_LOST = 2 };
+
+// Post a request's groups (task words words[k], w[0] = op | n << 32) and wait
+// for every answer.  LANE_DONE: answered (*errs: the frames with an error).
+// LANE_FALLBACK: not done by the lane, which has left: the caller does the
+// request on the launch path (*answered: groups the lane did finish before it
+// was given up — their outputs are written).  LANE_LOST: given up and the lane
+// did not leave in time: it may still write the request's buffers, so the
+// caller must not reuse them (the context is marked dead).
+LaneResult lane_run(wsg_ctx* c, LaneServer* s, const uint64_t (*words)[wsg::LANE_WORDS], uint32_t groups,
+                    uint64_t* errs, uint32_t* answered)
 {
-    wsg::LaneBell* b = c->lane.bell;
-    const uint64_t want = ++c->lane.seq;
-    // every unit a workgroup reads gets this request's tag, each after its
-    // value (x86 stores are seen in program order; the release stores keep
-    // the compiler's order): the group ranges (the caller's values), then
-    // the request words, the first one last (the lane polls its tag)
-    for (uint32_t k = 0; k < wsg::LANE_GROUPS_MAX; ++k)
-        for (int h = 0; h < 2; ++h)
-            __atomic_store_n(&b->grp[k][h].tag, want, __ATOMIC_RELEASE);
-    uint64_t w[wsg::LANE_WORDS] = {uint64_t(op) | (uint64_t(n) << 32), a[0], a[1], a[2], a[3], a[4], a[5],
-                                   uint64_t(G) | (uint64_t(c->lane_profile ? 1 : 0) << 32)};
-    for (uint32_t k = wsg::LANE_WORDS; k-- > 0;) {   // w[0] last: the lane polls its tag
-        b->w[k].v = w[k];
-        __atomic_store_n(&b->w[k].tag, want, __ATOMIC_RELEASE);
-    }
+    *errs = 0;
+    *answered = 0;
+    if (s->broken.load())
+        return LANE_FALLBACK;
+    const uint32_t W = s->W, R = wsg::LANE_RING;
+    const uint64_t x = s->tickets.fetch_add(groups);
+    s->inflight.fetch_add(1);
+    ++c->lane_requests;
     const auto t0 = std::chrono::steady_clock::now();
-    const uint32_t nw = c->lane_wgs;
-    uint32_t g = 0;   // workgroups [0, g) have answered
-    for (uint64_t i = 1;; ++i) {
-        while (g < nw && __atomic_load_n(&b->done[g], __ATOMIC_ACQUIRE) == want)
-            ++g;
-        if (g == nw) {
-            if (want % c->lane_reqs == 0)
-                c->lane.running = false;   // this launch ends after this request: the next call launches again
-            if (c->lane_profile) {
-                const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-                const double k = 1000.0 / double(c->wall_khz);   // us per tick
-                const uint64_t* v = b->prof;
-                c->lane_prof[1] += us;
-                c->lane_prof[3] += double(v[1] - v[0]) * k;
-                c->lane_prof[4] += double(v[2] - v[1]) * k;
-                c->lane_prof[5] += double(v[3] - v[2]) * k;
-                c->lane_prof[6] += double(v[4] - v[3]) * k;
-                c->lane_prof[7] += us - double(v[4] - v[0]) * k;
+    auto late = [&] { return std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(s->timeout_ms); };
+    // post: every group's slot (its previous task answered and read first),
+    // each unit's value then its tag, the first unit last
+    for (uint32_t k = 0; k < groups; ++k) {
+        const uint64_t tk = x + k;
+        const uint32_t wg = uint32_t(tk % W), slot = uint32_t((tk / W) % R);
+        if (tk >= uint64_t(W) * R) {
+            const uint64_t prev = tk - uint64_t(W) * R + 1;
+            for (uint64_t i = 1; s->released[wg * R + slot].load(std::memory_order_acquire) != prev; ++i) {
+                if ((i & 1023) == 0 && late()) {   // (posted anyway: the lane is stopped)
+                    lane_give_up(s);
+                    break;
+                }
+                __builtin_ia32_pause();
             }
-            return WSG_OK;
         }
+        wsg::LaneTask* T = &s->bell->box[wg][slot];
+        for (uint32_t u = wsg::LANE_WORDS; u-- > 0;) {
+            T->w[u].v = words[k][u];
+            __atomic_store_n(&T->w[u].tag, tk + 1, __ATOMIC_RELEASE);
+        }
+    }
+    lane_ensure_running(s);
+    // wait for the answers, group by group
+    uint32_t k = 0;
+    bool gave_up = false;
+    for (uint64_t i = 1; k < groups; ++i) {
+        while (k < groups) {
+            const uint64_t tk = x + k;
+            const uint32_t wg = uint32_t(tk % W), slot = uint32_t((tk / W) % R);
+            wsg::LaneResp& r = s->bell->resp[wg][slot];
+            if (__atomic_load_n(&r.done, __ATOMIC_ACQUIRE) != tk + 1)
+                break;
+            *errs += __atomic_load_n(&r.errs, __ATOMIC_RELAXED);
+            s->released[wg * R + slot].store(tk + 1, std::memory_order_release);
+            ++k;
+        }
+        if (k == groups)
+            break;
         if ((i & 255) == 0) {
-            bool left = false;
-            for (uint32_t k = 0; k < nw; ++k)
-                left = left || __atomic_load_n(&b->exited[k], __ATOMIC_ACQUIRE) == c->lane.gen;
-            if (left) {
-                // a workgroup of the running launch left (idle limit) before
-                // it saw this request: launch again, behind it on the
-                // stream (its other workgroups leave idle too); each new
-                // workgroup starts from its own `done` and takes its share
-                // if it is still owed
-                c->lane.running = false;
-                if (int rc = lane_start(c))
-                    return rc;
+            if (s->broken.load()) {
+                gave_up = true;
+                break;
             }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
-                c->lane.broken = true;
-                __atomic_store_n(&b->stop, 1u, __ATOMIC_RELEASE);
-                return WSG_EHIP;
+            lane_ensure_running(s);   // the launch announced its end before these tasks: the next one
+            if (late()) {
+                lane_give_up(s);
+                gave_up = true;
+                break;
             }
         }
         __builtin_ia32_pause();
     }
-}
-
-// Contexts of this process holding a lane (its doorbell allocated), and the
-// most it lets hold one ($WSG_LANE_CAP, default 4).  Every lane's
-// workgroups poll host memory over PCIe; with eight lanes (a TCP echo's four
-// server and four client threads) the polls cost more than the launches
-// they save: 100 clients 23.5 M msg/s with a lane per context, 30.3 M with
-// four, 39.4 M with none; one client 9.5 / 9.2 / 6.2 M; in memory, 100
-// clients on 4 threads 43.7 / 43.8 / 28.8 M (profiles/r4/lane_cap_ab.log).
-std::atomic<int>& lane_holders()
-{
-    static std::atomic<int> n{0};
-    return n;
-}
-
-// The lane for a request, launched if it is not running; nullptr when it
-// cannot be used (it did not answer before, its launch failed, or the
-// process holds its cap of lanes already).
-wsg::LaneBell* lane_ready(wsg_ctx* c)
-{
-    if (c->lane.broken || c->lane.declined)
-        return nullptr;
-    const bool fresh = !c->lane.bell;
-    if (fresh && lane_holders().fetch_add(1) >= c->lane_cap) {
-        lane_holders().fetch_sub(1);
-        c->lane.declined = true;
-        return nullptr;
+    if (!gave_up) {
+        s->inflight.fetch_sub(1);
+        return LANE_DONE;
     }
-    if (lane_start(c) != WSG_OK) {
-        if (fresh && !c->lane.bell)
-            lane_holders().fetch_sub(1);
-        return nullptr;
+    // Given up: nothing of the request may be touched until the lane has
+    // left (a workgroup that took a task before `stop` finishes it).
+    const bool drained = lane_drained(s, s->drain_ms);
+    for (uint32_t q = 0; q < groups; ++q) {
+        const uint64_t tk = x + q;
+        const uint32_t wg = uint32_t(tk % W), slot = uint32_t((tk / W) % R);
+        if (__atomic_load_n(&s->bell->resp[wg][slot].done, __ATOMIC_ACQUIRE) == tk + 1)
+            ++*answered;
+        s->released[wg * R + slot].store(tk + 1, std::memory_order_release);
     }
-    return c->lane.bell;
-}
-
-void lane_release(wsg_ctx* c)
-{
-    if (!c->lane.bell)
-        return;
-    lane_holders().fetch_sub(1);
-    {
-        std::lock_guard<std::mutex> g(lane_registry_lock());
-        auto& reg = lane_registry();
-        reg.erase(std::remove(reg.begin(), reg.end(), c), reg.end());
+    s->inflight.fetch_sub(1);
+    if (!drained) {
+        c->dead = true;
+        return LANE_LOST;
     }
-    if (!c->lane.broken)
-        lane_stop(c);
-    lane_report(c);
-    if (c->lane.stream)
-        (void)hipStreamDestroy(c->lane.stream);
-    if (!c->lane.running)   // (a lane that never answered may still read its doorbell)
-        (void)hipHostFree(c->lane.bell);
-    c->lane.bell = nullptr;
+    return LANE_FALLBACK;
 }
 
 } // namespace
@@ -653,110 +701,97 @@ const char* wsg_strerror(int code)
 }
 
 
+}   // extern "C"
+
+namespace {
+
+// The knobs a context takes from the environment, read once per context in
+// wsg_create (no environment read on any data path).
+struct Knobs {
+    bool check = false;             // $WSG_CHECK=1: checked launches (debug, see in_alloc)
+    uint64_t lane_max = 64 << 10;   // $WSG_LANE_MAX: largest lane request (0: the launch paths only)
+    uint32_t lane_groups = wsg::LANE_GROUPS_MAX;   // $WSG_LANE_GROUPS: most frame groups per lane request
+    uint64_t host_direct_max = 4 << 20;            // $WSG_HOST_DIRECT_MAX: host batches read in place up to this
+    uint64_t seg_bytes = 32ull << 20;              // $WSG_STAGE_MB: segment of the staged host pipelines
+    int enc_blocks_per_cu = 0;                     // $WSG_ENC_BLOCKS_PER_CU: k_encode_mask grid cap (0: default)
+    uint64_t enc_launch_pieces = 0;                // $WSG_ENC_LAUNCH_PIECES: pieces per k_encode_mask launch
+};
+
+Knobs read_knobs()
+{
+    Knobs k;
+    std::lock_guard<std::recursive_mutex> g(wsg::env_mutex());
+    if (const char* e = wsg::envp("WSG_CHECK"))
+        k.check = *e == '1';
+    if (const char* e = wsg::envp("WSG_LANE_MAX"))
+        k.lane_max = std::strtoull(e, nullptr, 10);
+    if (const char* e = wsg::envp("WSG_LANE_GROUPS")) {
+        const long v = std::atol(e);
+        if (v >= 1 && v <= long(wsg::LANE_GROUPS_MAX))
+            k.lane_groups = uint32_t(v);
+    }
+    if (const char* e = wsg::envp("WSG_HOST_DIRECT_MAX"))
+        k.host_direct_max = std::strtoull(e, nullptr, 10);
+    if (const char* e = wsg::envp("WSG_STAGE_MB"))
+        k.seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+    if (const char* e = wsg::envp("WSG_ENC_BLOCKS_PER_CU")) {   // (tests: grid-stride launch shapes)
+        const int v = std::atoi(e);
+        if (v > 0 && v <= 32768)
+            k.enc_blocks_per_cu = v;
+    }
+    if (const char* e = wsg::envp("WSG_ENC_LAUNCH_PIECES"))     // (tests: split launches)
+        k.enc_launch_pieces = std::strtoull(e, nullptr, 10);
+    return k;
+}
+
+} // namespace
+
+extern "C" {
+
 int wsg_create(int device, wsg_ctx** out)
 {
     if (!out)
         return WSG_EINVAL;
     *out = nullptr;
     wsg::hip_init_once();
-    std::lock_guard<std::recursive_mutex> env_guard(wsg::env_mutex());   // (wsg_env.h)
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || device < 0 || device >= count)
-        return WSG_EHIP;
-    wsg_ctx* c = new (std::nothrow) wsg_ctx();
-    if (!c)
-        return WSG_ENOMEM;
-    c->device = device;
+    const Knobs k = read_knobs();
+    wsg_ctx* c = nullptr;
     hipDeviceProp_t prop;
-    if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->d_err, sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(c->d_err, 0xFF, sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&c->d_err_host, sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(c->d_err_host, 0xFF, sizeof(unsigned long long)) != hipSuccess ||
-        hipDeviceSynchronize() != hipSuccess) {
+    {
+        // a device's first use edits the environment as the runtime's
+        // initialization does (wsg_env.h): these calls under the environment
+        // lock; the synchronize below, which waits for this stream only, not
+        std::lock_guard<std::recursive_mutex> env_guard(wsg::env_mutex());
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || device < 0 || device >= count)
+            return WSG_EHIP;
+        c = new (std::nothrow) wsg_ctx();
+        if (!c)
+            return WSG_ENOMEM;
+        c->device = device;
+        if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess ||
+            hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+            hipMalloc(&c->d_err, sizeof(unsigned long long)) != hipSuccess ||
+            hipMalloc(&c->d_err_host, sizeof(unsigned long long)) != hipSuccess) {
+            wsg_destroy(c);
+            return WSG_EHIP;
+        }
+    }
+    if (hipMemsetAsync(c->d_err, 0xFF, sizeof(unsigned long long), c->stream) != hipSuccess ||
+        hipMemsetAsync(c->d_err_host, 0xFF, sizeof(unsigned long long), c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
         wsg_destroy(c);
         return WSG_EHIP;
     }
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    if (const char* e = wsg::envp("WSG_BLOCKS_PER_CU")) {
-        const int v = std::atoi(e);
-        if (v > 0 && v <= 4096)
-            c->blocks_per_cu = c->dec_blocks_per_cu = c->enc_blocks_per_cu = v;   // A/B runs: every grid
-    }
-    if (const char* e = wsg::envp("WSG_XOR_DIRECT_MAX"))   // A/B measurements (per-call path)
-        c->xor_direct_max = std::strtoull(e, nullptr, 10);
-    if (const char* e = wsg::envp("WSG_HOST_DIRECT_MAX"))   // A/B measurements (small host batches)
-        c->host_direct_max = std::strtoull(e, nullptr, 10);
-    if (const char* e = wsg::envp("WSG_DEC_TILES_PER_BLOCK")) {   // A/B measurements (tools/tune.py)
-        const int v = std::atoi(e);
-        if (v >= 0 && v <= 64)
-            c->dec_tiles_per_block = v;
-    }
-    if (const char* e = wsg::envp("WSG_CHECK"))   // debug: checked launches (see in_alloc)
-        c->check = *e == '1';
-    if (const char* e = wsg::envp("WSG_ENC_BLOCKS_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
-        const int v = std::atoi(e);
-        if (v > 0 && v <= 32768)
-            c->enc_blocks_per_cu = v;
-    }
-    if (const char* e = wsg::envp("WSG_ENC_LAUNCH_PIECES"))   // A/B measurements (tools/c5_split.py)
-        c->enc_launch_pieces = std::strtoull(e, nullptr, 10);
-    if (const char* e = wsg::envp("WSG_FAN_WPB")) {   // A/B measurements (tools/c4_ab.py)
-        const int v = std::atoi(e);
-        if (v == 1 || v == 2 || v == 4 || v == 8 || v == 16)
-            c->fan_wpb = v;
-    }
-    if (const char* e = wsg::envp("WSG_FAN_WAVES_PER_CU")) {   // A/B measurements (tools/tune_enc.py)
-        const int v = std::atoi(e);
-        if (v > 0 && v <= 64)
-            c->fan_waves_per_cu = v;
-    }
-    if (const char* e = wsg::envp("WSG_FAN_GRID"))   // A/B measurements (tools/fan_many_ab.py)
-        c->fan_grid_min = uint32_t(std::strtoul(e, nullptr, 10));
-    if (const char* e = wsg::envp("WSG_SMALL_AVG"))   // A/B measurements (tools/tune_enc.py)
-        c->small_avg = std::strtoull(e, nullptr, 10);
-    if (const char* e = wsg::envp("WSG_LANE_MAX"))   // A/B measurements (tools/echo_size.py, bench_echo)
-        c->lane_max = std::strtoull(e, nullptr, 10);
-    if (const char* e = wsg::envp("WSG_LANE_PROFILE"))
-        c->lane_profile = *e == '1';
-    // default: one lane per hardware queue the runtime gives a priority
-    // ($GPU_MAX_HW_QUEUES, 4 unless set): past that, lanes share queues and
-    // each launch of one waits behind another's resident kernel (TCP echo,
-    // 4+4 threads: 26 M msg/s with 8 lanes on 4 queues, 55 M on 8 queues,
-    // profiles/r4/lane_hwq_ab.log)
-    if (const char* e = wsg::envp("GPU_MAX_HW_QUEUES")) {
-        const long v = std::atol(e);
-        if (v >= 1 && v <= 64)
-            c->lane_cap = int(v);
-    }
-    if (const char* e = wsg::envp("WSG_LANE_CAP")) {
-        const long v = std::atol(e);
-        if (v >= 1 && v <= (1l << 20))
-            c->lane_cap = int(v);
-    }
-    if (const char* e = wsg::envp("WSG_LANE_REQS")) {
-        const long v = std::atol(e);
-        if (v >= 1 && v <= (1l << 30))
-            c->lane_reqs = uint32_t(v);
-    }
-    if (const char* e = wsg::envp("WSG_TABLES_IN_PLACE"))
-        c->tables_in_place = *e != '0';
-    if (const char* e = wsg::envp("WSG_LANE_WGS")) {
-        const long v = std::atol(e);
-        if (v >= 1 && v <= long(wsg::LANE_WGS_MAX))
-            c->lane_wgs = uint32_t(v);
-    }
-    if (const char* e = wsg::envp("WSG_LANE_IDLE_US")) {
-        const long v = std::atol(e);
-        if (v > 0 && v <= 1000000)
-            c->lane_idle_us = uint32_t(v);
-    }
-    {
-        int khz = 0;
-        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
-            c->wall_khz = khz;
-    }
+    c->check = k.check;
+    c->lane_max = k.lane_max;
+    c->lane_groups = k.lane_groups;
+    c->host_direct_max = k.host_direct_max;
+    c->seg_bytes = k.seg_bytes;
+    if (k.enc_blocks_per_cu)
+        c->enc_blocks_per_cu = k.enc_blocks_per_cu;
+    c->enc_launch_pieces = k.enc_launch_pieces;
     *out = c;
     return WSG_OK;
 }
@@ -766,7 +801,6 @@ int wsg_destroy(wsg_ctx* c)
     if (!c)
         return WSG_EINVAL;
     (void)hipSetDevice(c->device);
-    lane_release(c);
     if (c->stream)
         (void)hipStreamSynchronize(c->stream);
     for (auto& ev : c->pending) {
@@ -859,8 +893,7 @@ int decode_launch(wsg_ctx* c, const uint8_t* d_wire, uint64_t wire_len, const ui
     // a short (or empty) wire are still checked
     const uint64_t tiles = ceil_div(wire_len, wsg::TILE);
     const int t = timing_begin(c, s);
-    const uint64_t units = c->dec_tiles_per_block ? ceil_div(tiles, uint64_t(c->dec_tiles_per_block)) : tiles;
-    WSG_HIP(wsg::launch_decode(s, grid_for(c, std::max(units, ceil_div(n, wsg::BLOCK)), c->dec_blocks_per_cu), d_wire, d_out, wire_len,
+    WSG_HIP(wsg::launch_decode(s, grid_for(c, std::max(tiles, ceil_div(n, wsg::BLOCK)), c->dec_blocks_per_cu), d_wire, d_out, wire_len,
                                d_frame_start, n, d_info, err));
     timing_end(c, s, t);
     return WSG_OK;
@@ -1120,17 +1153,39 @@ int wsg_xor_host(wsg_ctx* c, const void* src, void* dst, size_t len, uint32_t ke
     const wsg::TraceRange trace_range("wsg.xor_host");
     if (!c || (len && (!src || !dst)))
         return WSG_EINVAL;
+    if (c->dead)
+        return WSG_EHIP;
     if (len == 0)
         return WSG_OK;
     if (int rc = ensure_stage(c, len, 0))
         return rc;
-    hipStream_t s = c->stream;
     std::memcpy(c->h_stage, src, len);
+    if (len <= std::min<uint64_t>(c->lane_max, wsg::LANE_PSTAGE)) {
+        if (LaneServer* ls = lane_for(c)) {
+            // a message of the per-call path (PrepareSendFrame /
+            // PrepareReceiveFrame outside a batch scope): one lane task on the
+            // page-locked stage, no launch and no synchronize
+            const uint64_t w[1][wsg::LANE_WORDS] = {{wsg::LANE_XOR | (uint64_t(1) << 32),
+                                                     reinterpret_cast<uint64_t>(c->h_stage), uint64_t(len),
+                                                     uint64_t(key) | (uint64_t(phase & 3u) << 32), 0, 0,
+                                                     uint64_t(1) << 32, 0, 0}};
+            uint64_t errs = 0;
+            uint32_t answered = 0;
+            const LaneResult r = lane_run(c, ls, w, 1, &errs, &answered);
+            if (r == LANE_DONE) {
+                std::memcpy(dst, c->h_stage, len);
+                return WSG_OK;
+            }
+            if (r == LANE_LOST)
+                return WSG_EHIP;
+            std::memcpy(c->h_stage, src, len);   // (the lane has left: the launch path below, from the input)
+        }
+    }
+    hipStream_t s = c->stream;
     const uint64_t chunks = ceil_div(len, wsg::CHUNK);
     if (len <= c->xor_direct_max) {
-        // small payloads (a message of the per-call path): the kernel reads
-        // and writes the page-locked stage itself over PCIe, one launch and
-        // one sync instead of H2D + kernel + D2H
+        // small payloads: the kernel reads and writes the page-locked stage
+        // itself over PCIe, one launch and one sync instead of H2D + kernel + D2H
         WSG_HIP(wsg::launch_xor(s, grid_for(c, ceil_div(chunks, wsg::BLOCK)), c->h_stage, c->h_stage, len, key, phase));
     } else {
         WSG_HIP(hipMemcpyAsync(c->d_stage, c->h_stage, len, hipMemcpyHostToDevice, s));
@@ -1192,12 +1247,8 @@ struct Pipe {
 
 int pipe_for(wsg_ctx* c, wsg_ctx::Slot& sl, Pipe& p)
 {
-    const char* e = wsg::envp("WSG_PIPE");
-    p.roles = !(e && std::strcmp(e, "slots") == 0);
-    if (!p.roles) {
-        p.h2d = p.kern = p.d2h = sl.stream;
-        return WSG_OK;
-    }
+    (void)sl;
+    p.roles = true;
     for (hipStream_t* r : {&c->s_h2d, &c->s_kern, &c->s_d2h})
         if (!*r)
             WSG_HIP(hipStreamCreateWithFlags(r, hipStreamNonBlocking));
@@ -1350,53 +1401,55 @@ bool strictly_increasing(const uint64_t* v, uint32_t n)
 int decode_host_direct(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* frame_start, uint32_t n,
                        uint8_t* out, wsg_recv_info* info)
 {
-    const auto t_in = std::chrono::steady_clock::now();
     wsg_ctx::Slot& sl = c->slots[0];
     if (int rc = slot_reserve(sl, 0, n, false))
         return rc;
     // a table and records in wsg_host_alloc blocks (the batch classes') are
     // used where they are; others through the slot's page-locked copies
     const uint64_t* fs_dev = frame_start;
-    if (!c->tables_in_place || !in_host_block(frame_start, uint64_t(n) * sizeof(uint64_t))) {
+    if (!in_host_block(frame_start, uint64_t(n) * sizeof(uint64_t))) {
         std::memcpy(sl.h_fs, frame_start, size_t(n) * sizeof(uint64_t));
         fs_dev = sl.h_fs;
     }
     wsg_recv_info* info_dev =
-        c->tables_in_place && in_host_block(info, uint64_t(n) * sizeof(wsg_recv_info)) ? info : sl.h_info;
-    wsg::LaneBell* lb = nullptr;
-    if (wire_len <= std::min<uint64_t>(c->lane_max, wsg::LANE_STAGE - 64) && n > 0 && n <= lane_max_frames(c) &&
-        strictly_increasing(frame_start, n) && (lb = lane_ready(c))) {
-        // a few KiB (an echo's read): the resident lane, no launch; group
-        // k's wire range from its first start (0 for the first) to the next
-        // group's (wire_len after the last)
-        const uint32_t G = lane_group_size(c, n);
-        for (uint32_t k = 0, f = 0; f < n; ++k, f += G) {
-            lb->grp[k][0].v = k == 0 ? 0 : std::min(frame_start[f], wire_len);
-            lb->grp[k][1].v = f + G < n ? std::min(frame_start[f + G], wire_len) : wire_len;
+        in_host_block(info, uint64_t(n) * sizeof(wsg_recv_info)) ? info : sl.h_info;
+    LaneServer* ls = nullptr;
+    if (wire_len <= std::min<uint64_t>(c->lane_max, wsg::LANE_STAGE - 64) && n > 0 && n <= kLaneMaxFrames &&
+        strictly_increasing(frame_start, n) && (ls = lane_for(c))) {
+        // a few KiB (an echo's read): the device's resident lane, no launch;
+        // group k's wire range from its first start (0 for the first) to the
+        // next group's (wire_len after the last)
+        uint32_t groups = 0;
+        const uint32_t per = lane_split(c, ls, n, &groups);
+        uint64_t w[wsg::LANE_GROUPS_MAX][wsg::LANE_WORDS];
+        for (uint32_t k = 0; k < groups; ++k) {
+            const uint32_t f = k * per, cnt = std::min(per, n - f);
+            w[k][0] = wsg::LANE_DECODE | (uint64_t(n) << 32);
+            w[k][1] = reinterpret_cast<uint64_t>(wire);
+            w[k][2] = wire_len;
+            w[k][3] = reinterpret_cast<uint64_t>(fs_dev);
+            w[k][4] = reinterpret_cast<uint64_t>(out);
+            w[k][5] = reinterpret_cast<uint64_t>(info_dev);
+            w[k][6] = uint64_t(f) | (uint64_t(cnt) << 32);
+            w[k][7] = k == 0 ? 0 : std::min(frame_start[f], wire_len);
+            w[k][8] = f + cnt < n ? std::min(frame_start[f + cnt], wire_len) : wire_len;
         }
-        const uint64_t a[6] = {reinterpret_cast<uint64_t>(wire), wire_len, reinterpret_cast<uint64_t>(fs_dev),
-                               reinterpret_cast<uint64_t>(out), reinterpret_cast<uint64_t>(info_dev), 0};
-        const auto t_ring = std::chrono::steady_clock::now();
-        if (lane_call(c, wsg::LANE_DECODE, n, G, a) == WSG_OK) {
-            const auto t_back = std::chrono::steady_clock::now();
+        uint64_t errs = 0;
+        uint32_t answered = 0;
+        const LaneResult r = lane_run(c, ls, w, groups, &errs, &answered);
+        if (r == LANE_DONE) {
             if (info_dev != info)
                 std::memcpy(info, info_dev, size_t(n) * sizeof(wsg_recv_info));
             // no frame erred (the lane's count): nothing for the status pass to
             // find, and the records the GPU just wrote stay out of this core's
             // caches unless the caller reads them
-            uint64_t errs = 0;
-            for (uint32_t g = 0; g < c->lane_wgs; ++g)
-                errs += lb->errs[g];
-            const int rc = errs ? host_batch_status(c, wire, wire_len, frame_start, n, info) : WSG_OK;
-            if (c->lane_profile) {
-                using us = std::chrono::duration<double, std::micro>;
-                c->lane_prof[0] += us(t_ring - t_in).count();
-                c->lane_prof[2] += us(std::chrono::steady_clock::now() - t_back).count();
-                ++c->lane_prof_n;
-            }
-            return rc;
+            return errs ? host_batch_status(c, wire, wire_len, frame_start, n, info) : WSG_OK;
         }
-        // the lane did not answer: the launch path below (from now on always)
+        // given up on the lane: its answered groups have unmasked their bytes
+        // (in place: a second pass would mask them again), and a lane that did
+        // not leave may still write the buffers
+        if (r == LANE_LOST || (answered && out == wire))
+            return WSG_EHIP;
     }
     hipStream_t s = c->stream;
     if (int rc = decode_launch(c, wire, wire_len, fs_dev, n, out, info_dev, s, c->d_err_host))
@@ -1416,14 +1469,14 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
     try {   // no C++ exception leaves the ABI (host vectors: WSG_ENOMEM)
         if (!c || (wire_len && (!wire || !out)) || (n && (!frame_start || !info)))
             return WSG_EINVAL;
+        if (c->dead)
+            return WSG_EHIP;
         if (n == 0) {
             if (wire_len && out != wire)
                 std::memmove(out, wire, wire_len);
             return WSG_OK;
         }
-        uint64_t seg_bytes = 32ull << 20;
-        if (const char* e = wsg::envp("WSG_STAGE_MB"))
-            seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+        const uint64_t seg_bytes = c->seg_bytes;
         const bool in_pinned = host_pinned(wire), out_pinned = host_pinned(out);
         if (in_pinned && out_pinned && wire_len <= c->host_direct_max && aligned16(wire) && aligned16(out) &&
             host_direct(wire) && host_direct(out))
@@ -1568,7 +1621,8 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
     try {   // no C++ exception leaves the ABI (host vectors: WSG_ENOMEM)
         if (!c || !wire_off || (n && (!desc || !wire)) || (payload_len && !payload))
             return WSG_EINVAL;
-        const auto t_in = std::chrono::steady_clock::now();   // ($WSG_LANE_PROFILE)
+        if (c->dead)
+            return WSG_EHIP;
         // frame offsets on the host (the same arithmetic as k_encode_scan_*), so
         // that segments can be cut and copied back without a device round trip
         wire_off[0] = 0;
@@ -1583,9 +1637,7 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
             return WSG_ENOMEM;
         if (n == 0)
             return WSG_OK;
-        uint64_t seg_bytes = 32ull << 20;
-        if (const char* e = wsg::envp("WSG_STAGE_MB"))
-            seg_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+        const uint64_t seg_bytes = c->seg_bytes;
         const bool in_pinned = host_pinned(payload), out_pinned = host_pinned(wire);
         if (in_pinned && out_pinned && wire_off[n] <= c->host_direct_max && aligned16(wire) && n <= (1u << 20) &&
             host_direct(wire) && (payload_len == 0 || host_direct(payload))) {
@@ -1598,43 +1650,51 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
             // descriptors and offsets in wsg_host_alloc blocks (the batch
             // classes') are read where they are; others through copies
             const wsg_send_desc* desc_dev = desc;
-            if (!c->tables_in_place || !in_host_block(desc, uint64_t(n) * sizeof(wsg_send_desc))) {
+            if (!in_host_block(desc, uint64_t(n) * sizeof(wsg_send_desc))) {
                 std::memcpy(sl.h_desc, desc, size_t(n) * sizeof(wsg_send_desc));
                 desc_dev = sl.h_desc;
             }
-            wsg::LaneBell* lb = nullptr;
-            if (wire_off[n] <= c->lane_max && n <= lane_max_frames(c) && (lb = lane_ready(c))) {
-                // a few KiB (the replies of an echo's read): the resident
-                // lane at the offsets computed above, no launch; group k's
-                // payload span for its staging
+            LaneServer* ls = nullptr;
+            if (wire_off[n] <= c->lane_max && n <= kLaneMaxFrames && (ls = lane_for(c))) {
+                // a few KiB (the replies of an echo's read): the device's
+                // resident lane at the offsets computed above, no launch;
+                // group k's payload span for its staging
                 const uint64_t* off_dev = wire_off;
-                if (!c->tables_in_place || !in_host_block(wire_off, (uint64_t(n) + 1) * sizeof(uint64_t))) {
+                if (!in_host_block(wire_off, (uint64_t(n) + 1) * sizeof(uint64_t))) {
                     if (int rc = slot_reserve(sl, 0, uint64_t(n) + 1, false))
                         return rc;
                     std::memcpy(sl.h_fs, wire_off, (size_t(n) + 1) * sizeof(uint64_t));
                     off_dev = sl.h_fs;
                 }
-                const uint32_t G = lane_group_size(c, n);
-                for (uint32_t k = 0, f = 0; f < n; ++k, f += G) {
+                uint32_t groups = 0;
+                const uint32_t per = lane_split(c, ls, n, &groups);
+                uint64_t w[wsg::LANE_GROUPS_MAX][wsg::LANE_WORDS];
+                for (uint32_t k = 0; k < groups; ++k) {
+                    const uint32_t f = k * per, cnt = std::min(per, n - f);
                     uint64_t lo = UINT64_MAX, hi = 0;
-                    for (uint32_t i = f, e = std::min(n, f + G); i < e; ++i)
+                    for (uint32_t i = f; i < f + cnt; ++i)
                         if (desc[i].len) {
                             lo = std::min(lo, desc[i].src_off);
                             hi = std::max(hi, desc[i].src_off + desc[i].len);
                         }
-                    lb->grp[k][0].v = hi ? lo : 0;
-                    lb->grp[k][1].v = hi;
+                    w[k][0] = wsg::LANE_ENCODE | (uint64_t(n) << 32);
+                    w[k][1] = reinterpret_cast<uint64_t>(payload);
+                    w[k][2] = reinterpret_cast<uint64_t>(desc_dev);
+                    w[k][3] = reinterpret_cast<uint64_t>(off_dev);
+                    w[k][4] = reinterpret_cast<uint64_t>(wire);
+                    w[k][5] = 0;
+                    w[k][6] = uint64_t(f) | (uint64_t(cnt) << 32);
+                    w[k][7] = hi ? lo : 0;
+                    w[k][8] = hi;
                 }
-                const uint64_t a[6] = {reinterpret_cast<uint64_t>(payload), reinterpret_cast<uint64_t>(desc_dev),
-                                       reinterpret_cast<uint64_t>(off_dev), reinterpret_cast<uint64_t>(wire), 0, 0};
-                const auto t_ring = std::chrono::steady_clock::now();
-                if (lane_call(c, wsg::LANE_ENCODE, n, G, a) == WSG_OK) {
-                    if (c->lane_profile) {
-                        c->lane_prof[0] += std::chrono::duration<double, std::micro>(t_ring - t_in).count();
-                        ++c->lane_prof_n;
-                    }
+                uint64_t errs = 0;
+                uint32_t answered = 0;
+                const LaneResult r = lane_run(c, ls, w, groups, &errs, &answered);
+                if (r == LANE_DONE)
                     return WSG_OK;
-                }
+                if (r == LANE_LOST)
+                    return WSG_EHIP;   // (the lane may still write the frames)
+                // given up on the lane, which has left: the launch path writes every frame again
             }
             hipStream_t s = c->stream;
             if (int rc = encode_launch(c, s, payload, desc_dev, n, wire, wire_off[n], sl.d_woff, sl.enc,
@@ -1812,12 +1872,15 @@ int wsg_lane_stats(wsg_ctx* c, uint64_t* requests, uint64_t* launches, int* runn
 {
     if (!c)
         return WSG_EINVAL;
+    LaneServer* s = c->lane;
     if (requests)
-        *requests = c->lane.seq;
+        *requests = c->lane_requests;
     if (launches)
-        *launches = c->lane.launches;
-    if (running)
-        *running = c->lane.broken ? -1 : c->lane.running ? 1 : 0;
+        *launches = s ? s->launches.load() : 0;
+    if (running) {
+        const uint32_t g = s ? s->gen.load() : 0;
+        *running = !s ? 0 : s->broken.load() ? -1 : (g && __atomic_load_n(&s->bell->ctl.closing, __ATOMIC_ACQUIRE) != g) ? 1 : 0;
+    }
     return WSG_OK;
 }
 

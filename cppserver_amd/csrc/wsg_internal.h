@@ -103,16 +103,24 @@ hipError_t launch_rebase_offsets(hipStream_t s, const uint64_t* stage, const uin
 // Test hook only: one wave waiting `us` microseconds (at most 0.2 s) on `s`.
 hipError_t launch_test_spin(hipStream_t s, uint32_t us);
 
-// ---- the host lane: a resident one-workgroup kernel for small host batches
+// ---- the host lane: one resident kernel per device for small host batches
 // A host batch of a few KiB (an echo's read: ~1000 frames of 38 B) costs a
 // launch and a synchronize per pass (10 us for an empty kernel on MI355X,
 // tools/smallpass.hip) on top of its PCIe round trips.  The lane is launched
-// once and waits on a doorbell in page-locked host memory: the host writes a
-// request and its sequence number, the lane does it on the host buffers in
-// place and answers with the number; the host spins on the answer.  Every
-// wave of it ends: on `stop`, or after idle_ticks of the constant clock with
-// no request (the host launches it again when it next rings).
-enum : uint32_t { LANE_DECODE = 1, LANE_ENCODE = 2 };
+// once per device and shared by every context of the process: W workgroups,
+// each with a mailbox of LANE_RING task slots in page-locked host memory.
+// A request is cut into frame groups; group k gets the ticket x + k of a
+// process-wide ticket counter, i.e. slot (x + k) / W of workgroup (x + k) % W,
+// so consecutive requests spread over the workgroups and one request's groups
+// run side by side.  The host writes a slot's units (each value, then its
+// tag = ticket + 1; the first unit last), the workgroup polls the first unit
+// of its next slot, does the group on the host buffers in place and answers
+// in the slot's response.  Every workgroup ends: on `stop` (teardown, or a
+// request that timed out), or after idle_ticks without a task / yield_ticks of
+// running, announced in `closing` so that the others follow at their next
+// check; a caller waiting on an answer launches the next generation, which
+// resumes each mailbox where the last one left it (next_j).
+enum : uint32_t { LANE_DECODE = 1, LANE_ENCODE = 2, LANE_XOR = 3 };
 constexpr uint32_t LANE_THREADS = 1024;   // one workgroup; frames per group (lane per frame)
 constexpr uint64_t LANE_STAGE = 64 << 10;  // decode: wire bytes staged in LDS (the lane's batch limit)
 constexpr uint64_t LANE_PSTAGE = 64 << 10; // encode: payload arena staged in LDS when its 16-B blocks fit
@@ -123,40 +131,56 @@ constexpr uint64_t LANE_LDS_DECODE = LANE_STAGE + 60 * LANE_THREADS + 64;
 constexpr uint64_t LANE_LDS_ENCODE = 72 * LANE_THREADS + 64 + LANE_PSTAGE;
 constexpr uint64_t LANE_LDS = LANE_LDS_DECODE > LANE_LDS_ENCODE ? LANE_LDS_DECODE : LANE_LDS_ENCODE;
 static_assert(LANE_LDS <= 160 * 1024 - 1024, "the lane's workgroup LDS");
-constexpr uint32_t LANE_WGS_MAX = 16;          // workgroups of the lane (each a CU's worth of LDS)
+constexpr uint32_t LANE_WGS_MAX = 32;          // workgroups of the lane (each a CU's worth of LDS)
 constexpr uint32_t LANE_GROUPS_MAX = 32;       // frame groups of a request (<= 32 Ki frames)
-constexpr uint32_t LANE_GROUPS_PER_WG = 4;     // groups one workgroup takes (LANE_GROUPS_MAX / 8 workgroups)
-constexpr uint32_t LANE_WORDS = 8;             // request words (w[])
-// A request word and the number of the request it belongs to (the host
-// stores v, then tag; the lane reads the 16 bytes in one request).
+constexpr uint32_t LANE_RING = 64;             // task slots per workgroup mailbox
+constexpr uint32_t LANE_WORDS = 9;             // task units (w[])
+// A task word and the ticket it belongs to, + 1 (the host stores v, then
+// tag; the lane reads the 16 bytes in one request).
 struct alignas(16) LaneUnit {
     uint64_t v, tag;
 };
-struct LaneBell {
-    LaneUnit w[LANE_WORDS];                // host: op | n << 32, a[0..5], G | profile << 32
-    LaneUnit grp[LANE_GROUPS_MAX][2];      // host: group k's range (decode: wire [lo, hi); encode: payload span)
-    uint64_t done[LANE_WGS_MAX];           // lane: workgroup g's last request answered (its tag, release)
-    uint64_t errs[LANE_WGS_MAX];           // lane: frames with an error among workgroup g's (decode; before done)
-    uint64_t prof[8];                      // lane: workgroup 0's phase clocks ($WSG_LANE_PROFILE)
-    uint32_t stop;                         // host: leave now
-    uint32_t pad1[15];
-    uint32_t exited[LANE_WGS_MAX];         // lane: workgroup g of launch `gen` has left (its last store)
+// One frame group of a request (the host's, read by one workgroup):
+//   w[0] = op | n << 32 (posted last: the workgroup polls its tag)
+//   decode: w[1..5] = wire, wire_len, frame_start, out, info;
+//           w[6] = f_lo | cnt << 32 (the group's frames [f_lo, f_lo + cnt));
+//           w[7], w[8] = the group's wire range [lo, hi): its first start (0
+//           for the first group) to the next group's (wire_len after the last),
+//           clamped to wire_len — bit-identical to k_decode there; the table
+//           strictly increasing (the caller checks), wire_len + 64 <= LANE_STAGE
+//   encode: w[1..4] = payload, desc, wire_off (n + 1, host-computed), wire;
+//           w[6] = f_lo | cnt << 32; w[7], w[8] = the group's payload span
+//           [lo, hi) ({0, 0}: none)
+//   xor:    w[1..3] = buffer, length, key | phase << 32 (n = 1): the
+//           page-locked buffer XORed in place, byte i with key byte
+//           (phase + i) % 4
+struct LaneTask {
+    LaneUnit w[LANE_WORDS];
+    uint64_t pad[2];
 };
-// Request: G frames per group (1..LANE_THREADS), groups k = 0.. of frames
-// [k G, min(n, (k + 1) G)); workgroup g takes groups g, g + nw, ... (at most
-// LANE_GROUPS_PER_WG: the host picks G so).
-// decode: a = {wire, wire_len, frame_start, out, info}; the table strictly
-//         increasing (the caller checks), wire_len + 64 <= LANE_STAGE;
-//         grp[k] = {lo, hi}: k's first start (0 for k = 0) and the next
-//         group's (wire_len for the last), both clamped to wire_len —
-//         bit-identical to k_decode there
-// encode: a = {payload, desc, wire_off (n + 1, host-computed), wire};
-//         grp[k] = the payload span [lo, hi) of k's frames ({0, 0}: none)
-// A launch ends after idle_ticks without a request, on `stop`, or after
-// answering a request whose number is a multiple of `reqs` (gen: the
-// launch's number, >= 1, what its workgroups store in exited[]).
-hipError_t launch_lane(hipStream_t s, LaneBell* bell, uint32_t workgroups, uint64_t idle_ticks, uint32_t gen,
-                       uint32_t reqs);
+// The lane's answer to a task: errs (decode: frames with an error), then
+// done = the task's tag (release).
+struct alignas(16) LaneResp {
+    uint64_t done, errs;
+};
+struct alignas(16) LaneCtl {
+    uint32_t stop;      // host: every workgroup leaves at its next check
+    uint32_t closing;   // lane: launch `closing` is ending (its workgroups leave at their next check)
+    uint64_t pad;
+};
+struct LaneBell {
+    LaneCtl ctl;
+    uint64_t next_j[LANE_WGS_MAX];             // lane: workgroup g's next mailbox position (stored as it leaves)
+    LaneResp resp[LANE_WGS_MAX][LANE_RING];    // lane: answers
+    LaneTask box[LANE_WGS_MAX][LANE_RING];     // host: mailboxes (ticket x: box[x % W][(x / W) % LANE_RING])
+};
+// A launch of `workgroups` (the server's W) workgroups of generation `gen`
+// (>= 1): each leaves after idle_ticks without a task, after yield_ticks of
+// running (at a task boundary), on `stop`, or when `closing` names its
+// generation.  delay_ticks: a test hook, the workgroups wait that long before
+// their first poll (a lane that starts late).
+hipError_t launch_lane(hipStream_t s, LaneBell* bell, uint32_t workgroups, uint64_t idle_ticks,
+                       uint64_t yield_ticks, uint32_t gen, uint64_t delay_ticks);
 
 // HIP device a context is bound to (wsg_capi.hip)
 int ctx_device(const wsg_ctx* c);

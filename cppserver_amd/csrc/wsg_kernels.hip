@@ -44,9 +44,6 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_ENC_NT_HI
 #define WSG_ENC_NT_HI 1    // ... including the funnel's second block (the next lane's line)
 #endif
-#ifndef WSG_LANE_DIAG
-#define WSG_LANE_DIAG 0   // timing-only host lane diagnostics: 1 answer without the work, 2 per-frame phase only
-#endif
 #ifndef WSG_ENC_EDGE
 #define WSG_ENC_EDGE 2   // k_encode_mask non-data chunks: 2 vector build + dword stores (edge_chunk2), 1 the byte loop (edge_chunk, A/B): C3 0.730 -> 0.701 ms (profiles/r4/edge2_diag.log)
 #endif
@@ -1616,7 +1613,7 @@ struct LaneLoads {
 __device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload, uint64_t plo, uint64_t phi,
                                             const wsg_send_desc* __restrict__ desc, uint32_t f_lo, uint32_t cnt,
                                             const uint64_t* __restrict__ wire_off, uint8_t* __restrict__ wire,
-                                            uint8_t* lds, uint64_t* ts)
+                                            uint8_t* lds)
 {
     uint64_t* s_off = reinterpret_cast<uint64_t*>(lds);                             // LANE_THREADS + 1 (+1 pad)
     v4u* s_head = reinterpret_cast<v4u*>(lds + 8 * (LANE_THREADS + 2));
@@ -1647,19 +1644,15 @@ __device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload,
     dl.store(s_desc, 2 * uint64_t(cnt), true);
     pl.store(s_pay, pblocks, staged);
     __syncthreads();
-    ts[0] = wall_clock64();
     if (t < cnt) {
         const Desc d = load_desc(reinterpret_cast<const wsg_send_desc*>(s_desc) + t);
         (void)small_head(d, s_head[t], s_fr[t]);
     }
     __syncthreads();
-    ts[1] = wall_clock64();
-    if (WSG_LANE_DIAG != 2) {   // (DIAG 2, timing only: the per-frame phase alone)
-        if (staged)
-            small_chunks(payload, s_off, s_head, s_fr, cnt, wire, t, LANE_THREADS, StagedBlocks{s_pay, p0});
-        else
-            small_chunks(payload, s_off, s_head, s_fr, cnt, wire, t, LANE_THREADS);
-    }
+    if (staged)
+        small_chunks(payload, s_off, s_head, s_fr, cnt, wire, t, LANE_THREADS, StagedBlocks{s_pay, p0});
+    else
+        small_chunks(payload, s_off, s_head, s_fr, cnt, wire, t, LANE_THREADS);
 }
 
 // Decode of one frame group on the lane (frame table strictly increasing,
@@ -1676,7 +1669,7 @@ __device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload,
 __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, uint64_t wire_len, uint64_t lo,
                                             uint64_t hi, const uint64_t* __restrict__ fs, uint32_t n, uint32_t f_lo,
                                             uint32_t cnt, uint8_t* out, wsg_recv_info* __restrict__ info,
-                                            uint8_t* lds, uint64_t* ts, uint32_t* s_err)
+                                            uint8_t* lds, uint32_t* s_err)
 {
     v4u* s_wire = reinterpret_cast<v4u*>(lds);
     v4u* s_info = reinterpret_cast<v4u*>(lds + LANE_STAGE);                          // 2 blocks per record
@@ -1704,7 +1697,6 @@ __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, ui
         s_fs[cnt] = nx;
     wl.store(s_wire, wblocks, true);
     __syncthreads();
-    ts[0] = wall_clock64();   // (thread 0's of workgroup 0 is the one reported: $WSG_LANE_PROFILE)
     if (t < cnt) {
         const uint64_t st = s_fs[t];
         const uint64_t limit = s_fs[t + 1];   // the next frame's start, wire_len after the last
@@ -1719,14 +1711,11 @@ __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, ui
             atomicAdd(s_err, 1u);   // (the host skips its status pass over the records when no frame erred)
     }
     __syncthreads();
-    ts[1] = wall_clock64();
     {
         v4u* dst = reinterpret_cast<v4u*>(info + f_lo);
         for (uint32_t k = t; k < 2 * cnt; k += LANE_THREADS)
             dst[k] = s_info[k];
     }
-    if (WSG_LANE_DIAG == 2)   // timing only: the per-frame phase alone
-        return;
     for (uint64_t p = sb + uint64_t(t) * CHUNK; p < hi; p += uint64_t(LANE_THREADS) * CHUNK) {
         const v4u wv = s_wire[(p - sb) / CHUNK];
         // last frame whose payload starts at or before p (frame 0 if none)
@@ -1767,146 +1756,154 @@ __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, ui
     }
 }
 
-// The lane: gridDim.x workgroups, each polling the doorbell and taking the
-// frame groups g, g + nw, ... of every request (groups of `G` frames, the
-// host's per-group ranges in bell->grp), answering in its own done word.
-// The workgroups never wait on each other: each stages, works and answers
-// alone, so the request's PCIe reads and writes spread over nw CUs (one CU
-// has few requests in flight: one workgroup took ~5 us to stage a 38 KB
-// read and ~7 us to write it back, $WSG_LANE_PROFILE).
-__global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ bell, uint64_t idle_ticks, uint32_t gen,
-                                                       uint32_t reqs)
+// Per-call XOR on the lane: the page-locked buffer [buf, buf + len) XORed in
+// place, byte i with key byte (phase + i) % 4 (len <= LANE_PSTAGE, buf 16-B
+// aligned: the context's stage); every load issued before any is waited for.
+__device__ __forceinline__ void lane_xor(uint8_t* buf, uint64_t len, uint32_t key, uint32_t phase)
 {
-    __shared__ uint64_t s_tag;
-    __shared__ uint64_t s_w[LANE_WORDS];
-    __shared__ uint64_t s_g[LANE_GROUPS_PER_WG][2];
-    __shared__ int s_go;
-    __shared__ uint32_t s_err;   // the request's frames with an error (decode)
-    __shared__ v4u s_mem[LANE_LDS / 16];   // the op's staging (lane_decode / lane_encode layouts)
-    const uint32_t t = threadIdx.x, g = blockIdx.x, nw = gridDim.x;
-    uint64_t last = 0, seq = 0, t_seen = 0;
-    uint64_t ts[2] = {0, 0};
-    // the units this workgroup polls: lanes 0..7 the request words, 8..15
-    // the ranges of its groups g + j nw (j < LANE_GROUPS_PER_WG)
-    const LaneUnit* unit = nullptr;
-    if (t < LANE_WORDS) {
-        unit = &bell->w[t];
-    } else if (t < LANE_WORDS + 2 * LANE_GROUPS_PER_WG) {
-        const uint32_t j = (t - LANE_WORDS) >> 1, k = g + j * nw;
-        if (k < LANE_GROUPS_MAX)
-            unit = &bell->grp[k][(t - LANE_WORDS) & 1];
+    const uint32_t t = threadIdx.x;
+    const uint64_t chunks = len / CHUNK, tail = len & (CHUNK - 1);
+    LaneLoads<LANE_PSTAGE / CHUNK / LANE_THREADS> v;
+    v.load(buf, chunks, true);
+    const uint64_t q = chunks * CHUNK + t;
+    const uint32_t tb = t < tail ? uint32_t(buf[q]) : 0u;
+    const uint32_t kw = key_rot(key, phase);
+#pragma unroll
+    for (int u = 0; u < int(LANE_PSTAGE / CHUNK / LANE_THREADS); ++u) {
+        const uint64_t k = t + uint64_t(u) * LANE_THREADS;
+        if (k < chunks)
+            *reinterpret_cast<v4u*>(buf + k * CHUNK) = v.v[u] ^ kw;
     }
-    if (t < 64)
-        last = uni(__hip_atomic_load(&bell->done[g], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+    if (t < tail)
+        buf[q] = uint8_t(tb ^ key_byte(key, uint32_t(phase + q)));
+}
+
+// The lane: W = gridDim.x workgroups, workgroup g serving its mailbox
+// (bell->box[g]: the tickets g, g + W, g + 2W, ... in order).  Wave 0 polls
+// the first unit of the next slot; when it holds the slot's ticket, the
+// slot's units and the control word come in one round trip, and a `stop`
+// there means the task is NOT taken (a request the host gave up on: it waits
+// for the lane to leave before it uses the buffers itself).  The workgroups
+// never wait on each other: each stages, works and answers alone, so one
+// request's PCIe reads and writes spread over as many CUs as it has groups
+// (one CU has few requests in flight: one workgroup took ~5 us to stage a 38
+// KB read and ~7 us to write it back, round 4).
+__global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ bell, uint64_t idle_ticks,
+                                                       uint64_t yield_ticks, uint32_t gen, uint64_t delay_ticks)
+{
+    __shared__ uint64_t s_w[LANE_WORDS];
+    __shared__ int s_go;         // 1: a task in s_w; 0: leave
+    __shared__ uint32_t s_err;   // the task's frames with an error (decode)
+    __shared__ v4u s_mem[LANE_LDS / 16];   // the op's staging (lane_decode / lane_encode layouts)
+    const uint32_t t = threadIdx.x, g = blockIdx.x, W = gridDim.x;
+    uint64_t j = 0;     // (wave 0) this workgroup's mailbox position: ticket g + j W
+    uint32_t why = 0;   // (wave 0) why it leaves: 1 idle or yield (announced in `closing`), 2 stop, 3 closing seen
+    const LaneTask* box = bell->box[g];
+    const uint64_t t_start = wall_clock64();
+    if (t < 64) {
+        if (delay_ticks) {   // test hook: a lane that starts late (bounded: ~2^20 sleeps)
+            for (uint32_t i = 0; i < (1u << 20) && wall_clock64() - t_start < delay_ticks; ++i)
+                __builtin_amdgcn_s_sleep(64);
+        }
+        j = uni(__hip_atomic_load(&bell->next_j[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    }
     for (;;) {
         if (t < 64) {
-            // lane 0 of wave 0 polls the request's first word, which the
-            // host stores last (each unit: its value, then its tag; x86
-            // stores are seen in program order), so a new tag there means
-            // every unit of the request is written; then lanes 0..15 read
-            // the units this workgroup needs in one round trip.  (Polling
-            // all 16 units every time saved that round trip, ~2 us, but the
-            // lanes of four threads' contexts then kept PCIe busy with
-            // their polls: 100 echo clients on 4 threads 36 -> 17 M msg/s,
-            // profiles/r4/lane_poll_ab.log.)
+            const uint64_t want = uint64_t(g) + j * W + 1;
+            const LaneTask* task = &box[j % LANE_RING];
             int go = 0;
-            uint64_t val = 0;
+            if (wall_clock64() - t_start > yield_ticks)
+                why = 1;   // running long enough: step aside (calls that wait for the device to drain)
             const uint64_t t0 = wall_clock64();
             // at most ~2^22 polls of >= 1 us each: ends even if the clock stalls
-            for (uint32_t it = 0; it < (1u << 22); ++it) {
-                const v4u u = t == 0 ? ld16_sys(unit) : v4u{0, 0, 0, 0};
-                const uint64_t T = uni(uint64_t(u.z) | (uint64_t(u.w) << 32));
-                if (T != last) {
-                    __atomic_thread_fence(__ATOMIC_ACQUIRE);   // (system scope: the request's host buffers)
-                    seq = T;
+            for (uint32_t it = 0; !why && it < (1u << 22); ++it) {
+                const v4u u = t == 0 ? ld16_sys(&task->w[0]) : v4u{0, 0, 0, 0};
+                if (uni(uint64_t(u.z) | (uint64_t(u.w) << 32)) == want) {
                     go = 1;
                     break;
                 }
-                // (stop and the clock every 16th poll: each PCIe read is a
-                // round trip the next request would wait behind)
+                // (the control word and the clock every 16th poll: each PCIe
+                // read is a round trip the next task would wait behind)
                 if ((it & 15) == 15) {
-                    uint32_t quit = 0;
-                    if (t == 0)
-                        quit = __hip_atomic_load(&bell->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                               wall_clock64() - t0 > idle_ticks;
-                    if (uni(quit))
-                        break;
+                    const v4u c = t == 0 ? ld16_sys(&bell->ctl) : v4u{0, 0, 0, 0};
+                    const uint64_t now = wall_clock64();
+                    if (uni(c.x))
+                        why = 2;
+                    else if (uni(c.y) == gen)
+                        why = 3;   // another workgroup of this launch left: follow
+                    else if (now - t0 > idle_ticks || now - t_start > yield_ticks)
+                        why = 1;
                 }
-                __builtin_amdgcn_s_sleep(1);
+                if (it < 1024)
+                    __builtin_amdgcn_s_sleep(1);
+                else
+                    __builtin_amdgcn_s_sleep(8);   // idle for a while: poll host memory less often
             }
+            if (!go && !why)
+                why = 1;
             if (go) {
-                // the units, tags checked (always the new one: written
-                // before the first word's)
+                // every unit of the slot and the control word, one round trip;
+                // a unit still holding the slot's previous task (the reads may
+                // be served in any order): read again
+                const void* src = t < LANE_WORDS ? static_cast<const void*>(&task->w[t])
+                                                 : t == LANE_WORDS ? static_cast<const void*>(&bell->ctl) : nullptr;
+                uint64_t val = 0;
+                uint32_t stop = 0;
                 for (;;) {
-                    const v4u u = unit ? ld16_sys(unit) : v4u{0, 0, 0, 0};
-                    const uint64_t tag = uint64_t(u.z) | (uint64_t(u.w) << 32);
+                    const v4u u = src ? ld16_sys(src) : v4u{0, 0, 0, 0};
                     val = uint64_t(u.x) | (uint64_t(u.y) << 32);
-                    if (__ballot(unit && tag != seq) == 0)
+                    stop = u.x;
+                    const bool stale = t < LANE_WORDS && (uint64_t(u.z) | (uint64_t(u.w) << 32)) != want;
+                    if (__ballot(stale) == 0)
                         break;
                 }
-            }
-            if (go) {
-                if (t == 0)
-                    t_seen = wall_clock64();
-                if (t < LANE_WORDS)
+                __atomic_thread_fence(__ATOMIC_ACQUIRE);   // (system scope: the task's host buffers)
+                if (__builtin_amdgcn_readlane(stop, LANE_WORDS)) {
+                    why = 2;   // given up on by the host: not taken
+                    go = 0;
+                } else if (t < LANE_WORDS) {
                     s_w[t] = val;
-                else if (t < LANE_WORDS + 2 * LANE_GROUPS_PER_WG)
-                    s_g[(t - LANE_WORDS) >> 1][(t - LANE_WORDS) & 1] = unit ? val : 0;
+                }
             }
             if (t == 0) {
                 s_go = go;
-                s_tag = seq;
                 s_err = 0;
             }
         }
         __syncthreads();
         if (!s_go)
             break;
-        const uint32_t op = WSG_LANE_DIAG == 1 ? 0u : uint32_t(s_w[0]);   // DIAG 1: answer without the work (timing only)
+        const uint32_t op = uint32_t(s_w[0]);
         const uint32_t n = uint32_t(s_w[0] >> 32);
-        const uint32_t G = uint32_t(s_w[7]);   // frames per group, 1..LANE_THREADS
-        const bool profile = (s_w[7] >> 32) != 0;
+        const uint32_t f_lo = uint32_t(s_w[6]), cnt = uint32_t(s_w[6] >> 32);
         uint8_t* lds = reinterpret_cast<uint8_t*>(s_mem);
-        const uint32_t groups = G ? (n + G - 1) / G : 0;
-        for (uint32_t j = 0; op && j < LANE_GROUPS_PER_WG; ++j) {
-            const uint32_t k = g + j * nw;
-            if (k >= groups)
-                break;
-            const uint32_t f_lo = k * G, cnt = min(n - f_lo, G);
-            if (op == LANE_DECODE)
-                lane_decode(reinterpret_cast<const uint8_t*>(s_w[1]), s_w[2], s_g[j][0], s_g[j][1],
-                            reinterpret_cast<const uint64_t*>(s_w[3]), n, f_lo, cnt, reinterpret_cast<uint8_t*>(s_w[4]),
-                            reinterpret_cast<wsg_recv_info*>(s_w[5]), lds, ts, &s_err);
-            else if (op == LANE_ENCODE)
-                lane_encode(reinterpret_cast<const uint8_t*>(s_w[1]), s_g[j][0], s_g[j][1],
-                            reinterpret_cast<const wsg_send_desc*>(s_w[2]), f_lo, cnt,
-                            reinterpret_cast<const uint64_t*>(s_w[3]), reinterpret_cast<uint8_t*>(s_w[4]), lds, ts);
-            __syncthreads();   // the group's LDS is reused by the next
-        }
+        if (op == LANE_DECODE && cnt >= 1 && cnt <= LANE_THREADS)
+            lane_decode(reinterpret_cast<const uint8_t*>(s_w[1]), s_w[2], s_w[7], s_w[8],
+                        reinterpret_cast<const uint64_t*>(s_w[3]), n, f_lo, cnt, reinterpret_cast<uint8_t*>(s_w[4]),
+                        reinterpret_cast<wsg_recv_info*>(s_w[5]), lds, &s_err);
+        else if (op == LANE_ENCODE && cnt >= 1 && cnt <= LANE_THREADS)
+            lane_encode(reinterpret_cast<const uint8_t*>(s_w[1]), s_w[7], s_w[8],
+                        reinterpret_cast<const wsg_send_desc*>(s_w[2]), f_lo, cnt,
+                        reinterpret_cast<const uint64_t*>(s_w[3]), reinterpret_cast<uint8_t*>(s_w[4]), lds);
+        else if (op == LANE_XOR && s_w[2] <= LANE_PSTAGE)
+            lane_xor(reinterpret_cast<uint8_t*>(s_w[1]), s_w[2], uint32_t(s_w[3]), uint32_t(s_w[3] >> 32));
         __syncthreads();
         if (t == 0) {
-            const uint64_t t_work = wall_clock64();
-            __threadfence_system();   // the request's stores are visible to the host before its answer
-            if (profile && g == 0) {   // $WSG_LANE_PROFILE: the request's phases on the constant clock
-                const uint64_t t_fenced = wall_clock64();
-                const uint64_t v[5] = {t_seen, ts[0], ts[1], t_work, t_fenced};
-                for (int k = 0; k < 5; ++k)
-                    __hip_atomic_store(&bell->prof[k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            __hip_atomic_store(&bell->errs[g], uint64_t(s_err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&bell->done[g], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __threadfence_system();   // the task's stores are visible to the host before its answer
+            LaneResp* r = &bell->resp[g][j % LANE_RING];
+            __hip_atomic_store(&r->errs, uint64_t(s_err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&r->done, uint64_t(g) + j * W + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        last = seq;   // (wave 0's lanes: the tag they saw)
-        // every `reqs`-th request the lane ends after answering (all its
-        // workgroups at the same one): a running kernel holds up any call
-        // that waits for the device to drain (hipFree, hipHostFree, ...,
-        // from any thread), so a lane kept busy must still step aside; the
-        // host launches the next one behind it on the lane's stream
-        if (s_tag % reqs == 0)
-            break;
+        ++j;
     }
-    if (t == 0)   // (the launch's generation: a late store of an ended launch is not mistaken for this one's)
-        __hip_atomic_store(&bell->exited[g], gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == 0) {
+        // where the next launch resumes; then, leaving on its own, the launch
+        // announces it ends (the others follow; a waiting caller launches the
+        // next generation behind it on the lane's stream)
+        __hip_atomic_store(&bell->next_j[g], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (why == 1)
+            __hip_atomic_store(&bell->ctl.closing, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Grid = `main_blocks` streaming blocks, then the edge blocks.
@@ -2727,12 +2724,12 @@ hipError_t launch_test_spin(hipStream_t s, uint32_t us)
     return hipGetLastError();
 }
 
-hipError_t launch_lane(hipStream_t s, LaneBell* bell, uint32_t workgroups, uint64_t idle_ticks, uint32_t gen,
-                       uint32_t reqs)
+hipError_t launch_lane(hipStream_t s, LaneBell* bell, uint32_t workgroups, uint64_t idle_ticks,
+                       uint64_t yield_ticks, uint32_t gen, uint64_t delay_ticks)
 {
-    if (workgroups < 1 || workgroups > LANE_WGS_MAX || reqs == 0 || gen == 0)
+    if (workgroups < 1 || workgroups > LANE_WGS_MAX || gen == 0)
         return hipErrorInvalidValue;
-    k_lane<<<workgroups, LANE_THREADS, 0, s>>>(bell, idle_ticks, gen, reqs);
+    k_lane<<<workgroups, LANE_THREADS, 0, s>>>(bell, idle_ticks, yield_ticks, gen, delay_ticks);
     return hipGetLastError();
 }
 

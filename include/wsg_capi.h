@@ -336,17 +336,25 @@ int wsg_timing_minmax(wsg_ctx* ctx, double* min_ms, double* max_ms);
 
 /* ---- the host lane (measurement / test hook) ----------------------------- */
 /* Page-locked host batches of at most $WSG_LANE_MAX wire bytes (default 64
- * KiB) whose frame table is strictly increasing go to a resident kernel of
- * the context ($WSG_LANE_WGS workgroups, default 8, on a high-priority
- * stream) through a doorbell in host memory instead of a launch and a
- * synchronize per call (the C1 echo's reads).  A launch ends after
- * $WSG_LANE_IDLE_US (default 2000) without a request and after every
- * $WSG_LANE_REQS-th request (default 256: a running kernel holds up calls
- * that wait for the device to drain), and the next call launches it again.
- * At most $WSG_LANE_CAP contexts of a process (default: $GPU_MAX_HW_QUEUES,
- * else 4) hold a lane; the others take the launch paths.
- * Requests it answered, its launches, and whether it runs now (1), has left
- * (0) or stopped answering (-1: the launch paths from then on).            */
+ * KiB) whose frame table is strictly increasing, and wsg_xor_host calls of at
+ * most that many bytes, go to the device's resident lane instead of a launch
+ * and a synchronize per call (the C1 echo's reads; the per-call path).  One
+ * lane per device serves every context of the process: $WSG_LANE_WGS
+ * workgroups (default 8) on a high-priority stream, a mailbox each in host
+ * memory; a request is cut into at most $WSG_LANE_GROUPS frame groups (one
+ * per idle workgroup).  A launch ends after $WSG_LANE_IDLE_US (default 2000)
+ * without a task and after $WSG_LANE_YIELD_US (default 2000) of running (a
+ * running kernel holds up calls that wait for the device to drain); the next
+ * call launches it again.  A request unanswered for $WSG_LANE_TIMEOUT_MS
+ * (default 5000) gives the lane up for the process: the caller waits up to
+ * $WSG_LANE_DRAIN_MS (default 2000) for it to leave and then takes the
+ * launch path, or, if it does not leave, returns WSG_EHIP without touching
+ * the buffers (the lane may still write them) and the context returns
+ * WSG_EHIP from then on.  The lane's settings are read when a process first
+ * uses a device's lane.
+ * Requests this context put on the lane, the launches of the device's lane,
+ * and whether it runs now (1), has left (0) or was given up (-1: the launch
+ * paths from then on).                                                      */
 int wsg_lane_stats(wsg_ctx* ctx, uint64_t* requests, uint64_t* launches, int* running);
 
 #ifdef __cplusplus
