@@ -11,6 +11,7 @@
 #include "server/ws/ws_session.h"
 
 #include <algorithm>
+#include <thread>
 
 namespace CppServer {
 namespace WS {
@@ -48,9 +49,18 @@ bool receive_message(std::vector<uint8_t>& out, Required required, Prepare prepa
 
 void WSClient::ResetBuffers()
 {
-    if (WSReceiveBatch* b = _rx_batch.load(std::memory_order_acquire))
-        b->Clear(*this);   // message state resets in delivery order
-    else if (BatchScope::Active())
+    {
+        std::scoped_lock<QueueLock> use(_rx_use);
+        if (WSReceiveBatch* b = _rx_batch.load(std::memory_order_acquire)) {
+            b->Clear(*this);   // message state resets in delivery order
+            return;
+        }
+        if (_rx_draining) {
+            _rx_prev->Clear(*this);   // after the frames still queued in the batch being left
+            return;
+        }
+    }
+    if (BatchScope::Active())
         BatchScope::Receive().Clear(*this);
     else
         ClearWSBuffers();
@@ -65,10 +75,24 @@ WSClient::~WSClient()
 void WSClient::SetReceiveBatch(WSReceiveBatch* batch)
 {
     // swapped atomically (the IO thread reads it per read); the old batch
-    // drops this connection's frames after the swap
-    WSReceiveBatch* old = _rx_batch.exchange(batch, std::memory_order_acq_rel);
-    if (old && old != batch)
-        old->Forget(*this);
+    // delivers this connection's queued frames before its next read is taken
+    WSReceiveBatch* old;
+    {
+        std::scoped_lock<QueueLock> use(_rx_use);   // (a read still feeding the old batch finishes first)
+        old = _rx_batch.exchange(batch, std::memory_order_acq_rel);
+        if (old && old != batch) {
+            _rx_prev = old;
+            _rx_draining = true;
+        }
+    }
+    if (old && old != batch) {
+        // the frames this connection queued there are delivered before any
+        // later read of it goes the new way (reads wait meanwhile)
+        old->Drain(*this);
+        std::scoped_lock<QueueLock> use(_rx_use);
+        _rx_draining = false;
+        _rx_prev = nullptr;
+    }
 }
 
 bool WSClient::Connect()
@@ -142,9 +166,20 @@ void WSClient::onReceived(const void* buffer, size_t size)
 
 void WSClient::RouteFrames(const void* buffer, size_t size)
 {
-    if (WSReceiveBatch* b = _rx_batch.load(std::memory_order_acquire)) {
-        b->Feed(*this, buffer, size);
-    } else if (BatchScope::Active()) {
+    for (;;) {
+        {
+            std::scoped_lock<QueueLock> use(_rx_use);   // (SetReceiveBatch waits for this feed)
+            if (!_rx_draining) {
+                if (WSReceiveBatch* b = _rx_batch.load(std::memory_order_acquire)) {
+                    b->Feed(*this, buffer, size);
+                    return;
+                }
+                break;
+            }
+        }
+        std::this_thread::yield();   // a batch switch delivers this connection's earlier frames first
+    }
+    if (BatchScope::Active()) {
         BatchScope::Receive().Feed(*this, buffer, size);
         BatchScope::CheckLimits();
     } else {
@@ -156,7 +191,7 @@ void WSClient::SetSendBatch(WSSendBatch* batch)
 {
     WSSendBatch* old;
     {
-        std::scoped_lock locker(_ws_send_lock);
+        std::scoped_lock locker(_ws_send_lock, _tx_use);
         old = _tx_batch.exchange(batch, std::memory_order_acq_rel);
     }
     // not under the send lock: Forget may wait for a flush on another thread
@@ -168,9 +203,15 @@ void WSClient::SetSendBatch(WSSendBatch* batch)
 size_t WSClient::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status,
                            const CppCommon::Timespan* timeout)
 {
-    if (WSSendBatch* b = _tx_batch.load(std::memory_order_acquire))
-        b->Flush();   // earlier async frames go first
-    else if (BatchScope::Active())
+    bool batched = false;
+    {
+        std::scoped_lock<QueueLock> use(_tx_use);   // (SetSendBatch waits for this flush)
+        if (WSSendBatch* b = _tx_batch.load(std::memory_order_acquire)) {
+            b->Flush();   // earlier async frames go first
+            batched = true;
+        }
+    }
+    if (!batched && BatchScope::Active())
         BatchScope::Send().Flush();
     std::scoped_lock locker(_ws_send_lock);
     PrepareSendFrame(opcode, true, buffer, size, status);
@@ -254,9 +295,18 @@ std::vector<uint8_t> WSClient::ReceiveBinary(const CppCommon::Timespan& timeout)
 
 void WSSession::ResetBuffers()
 {
-    if (WSReceiveBatch* b = _rx_batch.load(std::memory_order_acquire))
-        b->Clear(*this);   // message state resets in delivery order
-    else if (BatchScope::Active())
+    {
+        std::scoped_lock<QueueLock> use(_rx_use);
+        if (WSReceiveBatch* b = _rx_batch.load(std::memory_order_acquire)) {
+            b->Clear(*this);   // message state resets in delivery order
+            return;
+        }
+        if (_rx_draining) {
+            _rx_prev->Clear(*this);   // after the frames still queued in the batch being left
+            return;
+        }
+    }
+    if (BatchScope::Active())
         BatchScope::Receive().Clear(*this);
     else
         ClearWSBuffers();
@@ -271,10 +321,24 @@ WSSession::~WSSession()
 void WSSession::SetReceiveBatch(WSReceiveBatch* batch)
 {
     // swapped atomically (the IO thread reads it per read); the old batch
-    // drops this connection's frames after the swap
-    WSReceiveBatch* old = _rx_batch.exchange(batch, std::memory_order_acq_rel);
-    if (old && old != batch)
-        old->Forget(*this);
+    // delivers this connection's queued frames before its next read is taken
+    WSReceiveBatch* old;
+    {
+        std::scoped_lock<QueueLock> use(_rx_use);   // (a read still feeding the old batch finishes first)
+        old = _rx_batch.exchange(batch, std::memory_order_acq_rel);
+        if (old && old != batch) {
+            _rx_prev = old;
+            _rx_draining = true;
+        }
+    }
+    if (old && old != batch) {
+        // the frames this connection queued there are delivered before any
+        // later read of it goes the new way (reads wait meanwhile)
+        old->Drain(*this);
+        std::scoped_lock<QueueLock> use(_rx_use);
+        _rx_draining = false;
+        _rx_prev = nullptr;
+    }
 }
 
 bool WSSession::Connect()
@@ -331,9 +395,20 @@ void WSSession::onReceived(const void* buffer, size_t size)
 
 void WSSession::RouteFrames(const void* buffer, size_t size)
 {
-    if (WSReceiveBatch* b = _rx_batch.load(std::memory_order_acquire)) {
-        b->Feed(*this, buffer, size);
-    } else if (BatchScope::Active()) {
+    for (;;) {
+        {
+            std::scoped_lock<QueueLock> use(_rx_use);   // (SetReceiveBatch waits for this feed)
+            if (!_rx_draining) {
+                if (WSReceiveBatch* b = _rx_batch.load(std::memory_order_acquire)) {
+                    b->Feed(*this, buffer, size);
+                    return;
+                }
+                break;
+            }
+        }
+        std::this_thread::yield();   // a batch switch delivers this connection's earlier frames first
+    }
+    if (BatchScope::Active()) {
         BatchScope::Receive().Feed(*this, buffer, size);
         BatchScope::CheckLimits();
     } else {
@@ -345,7 +420,7 @@ void WSSession::SetSendBatch(WSSendBatch* batch)
 {
     WSSendBatch* old;
     {
-        std::scoped_lock locker(_ws_send_lock);
+        std::scoped_lock locker(_ws_send_lock, _tx_use);
         old = _tx_batch.exchange(batch, std::memory_order_acq_rel);
     }
     // not under the send lock: Forget may wait for a flush on another thread
@@ -357,9 +432,15 @@ void WSSession::SetSendBatch(WSSendBatch* batch)
 size_t WSSession::SendFrame(uint8_t opcode, const void* buffer, size_t size, int status,
                             const CppCommon::Timespan* timeout)
 {
-    if (WSSendBatch* b = _tx_batch.load(std::memory_order_acquire))
-        b->Flush();   // earlier async frames go first
-    else if (BatchScope::Active())
+    bool batched = false;
+    {
+        std::scoped_lock<QueueLock> use(_tx_use);   // (SetSendBatch waits for this flush)
+        if (WSSendBatch* b = _tx_batch.load(std::memory_order_acquire)) {
+            b->Flush();   // earlier async frames go first
+            batched = true;
+        }
+    }
+    if (!batched && BatchScope::Active())
         BatchScope::Send().Flush();
     std::scoped_lock locker(_ws_send_lock);
     PrepareSendFrame(opcode, false, buffer, size, status);

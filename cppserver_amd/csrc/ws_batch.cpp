@@ -235,6 +235,27 @@ void WSReceiveBatch::Forget(WebSocket& ws)
     _waiters.fetch_sub(1, std::memory_order_relaxed);
 }
 
+void WSReceiveBatch::Drain(WebSocket& ws)
+{
+    for (;;) {
+        {
+            std::scoped_lock locker(_lock);
+            if (_flushing && _flusher == std::this_thread::get_id())
+                return;   // (a callback of this thread's flush: the rest goes with a later flush)
+            bool queued = false;
+            for (const Rec& r : _cur.recs)
+                if (r.ws == &ws) {
+                    queued = true;
+                    break;
+                }
+            if (!queued && !_flushing)
+                return;
+        }
+        if (Flush() == 0)
+            std::this_thread::yield();   // another thread's flush is delivering: wait for it to end
+    }
+}
+
 void WSReceiveBatch::ApplyPending(size_t from)
 {
     // the flushing thread, _lock held

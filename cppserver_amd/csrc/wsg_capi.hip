@@ -1159,16 +1159,21 @@ int wsg_xor_host(wsg_ctx* c, const void* src, void* dst, size_t len, uint32_t ke
         return WSG_OK;
     if (int rc = ensure_stage(c, len, 0))
         return rc;
-    std::memcpy(c->h_stage, src, len);
     if (len <= std::min<uint64_t>(c->lane_max, wsg::LANE_PSTAGE)) {
         if (LaneServer* ls = lane_for(c)) {
             // a message of the per-call path (PrepareSendFrame /
             // PrepareReceiveFrame outside a batch scope): one lane task on the
-            // page-locked stage, no launch and no synchronize
-            const uint64_t w[1][wsg::LANE_WORDS] = {{wsg::LANE_XOR | (uint64_t(1) << 32),
-                                                     reinterpret_cast<uint64_t>(c->h_stage), uint64_t(len),
-                                                     uint64_t(key) | (uint64_t(phase & 3u) << 32), 0, 0,
-                                                     uint64_t(1) << 32, 0, 0}};
+            // page-locked stage, no launch and no synchronize; a payload of
+            // up to LANE_INLINE bytes (an echo's 32) travels in the task
+            uint64_t w[1][wsg::LANE_WORDS] = {{wsg::LANE_XOR | (uint64_t(1) << 32),
+                                               reinterpret_cast<uint64_t>(c->h_stage), uint64_t(len),
+                                               uint64_t(key) | (uint64_t(phase & 3u) << 32), 0, 0, 0, 0, 0}};
+            if (len <= wsg::LANE_INLINE) {
+                w[0][0] = wsg::LANE_XOR_INLINE | (uint64_t(1) << 32);
+                std::memcpy(&w[0][4], src, len);
+            } else {
+                std::memcpy(c->h_stage, src, len);
+            }
             uint64_t errs = 0;
             uint32_t answered = 0;
             const LaneResult r = lane_run(c, ls, w, 1, &errs, &answered);
@@ -1178,9 +1183,10 @@ int wsg_xor_host(wsg_ctx* c, const void* src, void* dst, size_t len, uint32_t ke
             }
             if (r == LANE_LOST)
                 return WSG_EHIP;
-            std::memcpy(c->h_stage, src, len);   // (the lane has left: the launch path below, from the input)
+            // (the lane has left: the launch path below, from the input)
         }
     }
+    std::memcpy(c->h_stage, src, len);
     hipStream_t s = c->stream;
     const uint64_t chunks = ceil_div(len, wsg::CHUNK);
     if (len <= c->xor_direct_max) {

@@ -113,14 +113,15 @@ hipError_t launch_test_spin(hipStream_t s, uint32_t us);
 // process-wide ticket counter, i.e. slot (x + k) / W of workgroup (x + k) % W,
 // so consecutive requests spread over the workgroups and one request's groups
 // run side by side.  The host writes a slot's units (each value, then its
-// tag = ticket + 1; the first unit last), the workgroup polls the first unit
-// of its next slot, does the group on the host buffers in place and answers
+// tag = ticket + 1; the first unit last), the workgroup polls its next slot
+// (every unit in one read), does the group on the host buffers in place and answers
 // in the slot's response.  Every workgroup ends: on `stop` (teardown, or a
 // request that timed out), or after idle_ticks without a task / yield_ticks of
 // running, announced in `closing` so that the others follow at their next
 // check; a caller waiting on an answer launches the next generation, which
 // resumes each mailbox where the last one left it (next_j).
-enum : uint32_t { LANE_DECODE = 1, LANE_ENCODE = 2, LANE_XOR = 3 };
+enum : uint32_t { LANE_DECODE = 1, LANE_ENCODE = 2, LANE_XOR = 3, LANE_XOR_INLINE = 4 };
+constexpr uint64_t LANE_INLINE = 40;     // xor: payloads up to this size travel in the task (w[4..8])
 constexpr uint32_t LANE_THREADS = 1024;   // one workgroup; frames per group (lane per frame)
 constexpr uint64_t LANE_STAGE = 64 << 10;  // decode: wire bytes staged in LDS (the lane's batch limit)
 constexpr uint64_t LANE_PSTAGE = 64 << 10; // encode: payload arena staged in LDS when its 16-B blocks fit
@@ -153,7 +154,8 @@ struct alignas(16) LaneUnit {
 //           [lo, hi) ({0, 0}: none)
 //   xor:    w[1..3] = buffer, length, key | phase << 32 (n = 1): the
 //           page-locked buffer XORed in place, byte i with key byte
-//           (phase + i) % 4
+//           (phase + i) % 4; LANE_XOR_INLINE: the payload (<= LANE_INLINE
+//           bytes) in w[4..8], the result written to the buffer
 struct LaneTask {
     LaneUnit w[LANE_WORDS];
     uint64_t pad[2];

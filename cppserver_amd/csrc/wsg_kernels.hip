@@ -1780,10 +1780,9 @@ __device__ __forceinline__ void lane_xor(uint8_t* buf, uint64_t len, uint32_t ke
 
 // The lane: W = gridDim.x workgroups, workgroup g serving its mailbox
 // (bell->box[g]: the tickets g, g + W, g + 2W, ... in order).  Wave 0 polls
-// the first unit of the next slot; when it holds the slot's ticket, the
-// slot's units and the control word come in one round trip, and a `stop`
-// there means the task is NOT taken (a request the host gave up on: it waits
-// for the lane to leave before it uses the buffers itself).  The workgroups
+// the next slot's units and the control word, all in one round trip; a
+// `stop` there means no task is taken (a request the host gave up on: it
+// waits for the lane to leave before it uses the buffers itself).  The workgroups
 // never wait on each other: each stages, works and answers alone, so one
 // request's PCIe reads and writes spread over as many CUs as it has groups
 // (one CU has few requests in flight: one workgroup took ~5 us to stage a 38
@@ -1815,23 +1814,43 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
             if (wall_clock64() - t_start > yield_ticks)
                 why = 1;   // running long enough: step aside (calls that wait for the device to drain)
             const uint64_t t0 = wall_clock64();
+            // every poll reads all of the slot's units and the control word in
+            // one round trip (lanes 0..LANE_WORDS): a task is taken the moment
+            // its first unit shows, with no second read.  (A unit still
+            // holding the slot's previous task — the reads may be served in
+            // any order — is read again; the control word read with a task's
+            // first unit: a `stop` set after it is covered by the host, which
+            // waits for the lane to leave before it touches the buffers.)
+            const void* src = t < LANE_WORDS ? static_cast<const void*>(&task->w[t])
+                                             : t == LANE_WORDS ? static_cast<const void*>(&bell->ctl) : nullptr;
+            uint64_t val = 0;
             // at most ~2^22 polls of >= 1 us each: ends even if the clock stalls
             for (uint32_t it = 0; !why && it < (1u << 22); ++it) {
-                const v4u u = t == 0 ? ld16_sys(&task->w[0]) : v4u{0, 0, 0, 0};
-                if (uni(uint64_t(u.z) | (uint64_t(u.w) << 32)) == want) {
-                    go = 1;
+                const v4u u = src ? ld16_sys(src) : v4u{0, 0, 0, 0};
+                val = uint64_t(u.x) | (uint64_t(u.y) << 32);
+                const uint64_t tag = uint64_t(u.z) | (uint64_t(u.w) << 32);
+                const uint32_t stop = __builtin_amdgcn_readlane(u.x, LANE_WORDS);
+                const uint32_t closing = __builtin_amdgcn_readlane(u.y, LANE_WORDS);
+                if (stop) {
+                    why = 2;   // given up on by the host (or teardown): no task taken
                     break;
                 }
-                // (the control word and the clock every 16th poll: each PCIe
-                // read is a round trip the next task would wait behind)
+                if (closing == gen) {
+                    why = 3;   // another workgroup of this launch left: follow
+                    break;
+                }
+                const uint64_t tag0 = uint64_t(__builtin_amdgcn_readlane(u.z, 0)) |
+                                      (uint64_t(__builtin_amdgcn_readlane(u.w, 0)) << 32);
+                if (tag0 == want) {
+                    if (__ballot(t < LANE_WORDS && tag != want) == 0) {
+                        go = 1;
+                        break;
+                    }
+                    continue;   // (part of the slot still the old task: again, at once)
+                }
                 if ((it & 15) == 15) {
-                    const v4u c = t == 0 ? ld16_sys(&bell->ctl) : v4u{0, 0, 0, 0};
                     const uint64_t now = wall_clock64();
-                    if (uni(c.x))
-                        why = 2;
-                    else if (uni(c.y) == gen)
-                        why = 3;   // another workgroup of this launch left: follow
-                    else if (now - t0 > idle_ticks || now - t_start > yield_ticks)
+                    if (now - t0 > idle_ticks || now - t_start > yield_ticks)
                         why = 1;
                 }
                 if (it < 1024)
@@ -1842,28 +1861,9 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
             if (!go && !why)
                 why = 1;
             if (go) {
-                // every unit of the slot and the control word, one round trip;
-                // a unit still holding the slot's previous task (the reads may
-                // be served in any order): read again
-                const void* src = t < LANE_WORDS ? static_cast<const void*>(&task->w[t])
-                                                 : t == LANE_WORDS ? static_cast<const void*>(&bell->ctl) : nullptr;
-                uint64_t val = 0;
-                uint32_t stop = 0;
-                for (;;) {
-                    const v4u u = src ? ld16_sys(src) : v4u{0, 0, 0, 0};
-                    val = uint64_t(u.x) | (uint64_t(u.y) << 32);
-                    stop = u.x;
-                    const bool stale = t < LANE_WORDS && (uint64_t(u.z) | (uint64_t(u.w) << 32)) != want;
-                    if (__ballot(stale) == 0)
-                        break;
-                }
                 __atomic_thread_fence(__ATOMIC_ACQUIRE);   // (system scope: the task's host buffers)
-                if (__builtin_amdgcn_readlane(stop, LANE_WORDS)) {
-                    why = 2;   // given up on by the host: not taken
-                    go = 0;
-                } else if (t < LANE_WORDS) {
+                if (t < LANE_WORDS)
                     s_w[t] = val;
-                }
             }
             if (t == 0) {
                 s_go = go;
@@ -1887,6 +1887,13 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
                         reinterpret_cast<const uint64_t*>(s_w[3]), reinterpret_cast<uint8_t*>(s_w[4]), lds);
         else if (op == LANE_XOR && s_w[2] <= LANE_PSTAGE)
             lane_xor(reinterpret_cast<uint8_t*>(s_w[1]), s_w[2], uint32_t(s_w[3]), uint32_t(s_w[3] >> 32));
+        else if (op == LANE_XOR_INLINE && s_w[2] <= LANE_INLINE && t < (s_w[2] + 3) / 4) {
+            // the payload came with the task (w[4..8]): one dword per lane,
+            // written to the buffer (rounded up to whole dwords: the stage
+            // has the room), no read of host memory
+            const uint32_t d = uint32_t(s_w[4 + t / 2] >> (32 * (t & 1)));
+            reinterpret_cast<uint32_t*>(s_w[1])[t] = d ^ key_rot(uint32_t(s_w[3]), uint32_t(s_w[3] >> 32));
+        }
         __syncthreads();
         if (t == 0) {
             __threadfence_system();   // the task's stores are visible to the host before its answer

@@ -85,7 +85,10 @@ private:
 //! A growable array of trivially copyable records in page-locked memory
 //! (wsg_host_alloc): a batch's frame table, records and descriptors, which
 //! the GPU pass then reads and writes where they are instead of through a
-//! staging copy.
+//! staging copy.  Growing keeps the old block until the array is destroyed:
+//! a grow happens under the batch's queue lock, and freeing page-locked memory
+//! waits for the device to drain (a resident lane hands over every few ms), so
+//! no free runs there.  The kept blocks total less than the live one.
 template <class T>
 class PinnedArray
 {
@@ -95,18 +98,25 @@ public:
     PinnedArray() = default;
     PinnedArray(const PinnedArray&) = delete;
     PinnedArray& operator=(const PinnedArray&) = delete;
-    PinnedArray(PinnedArray&& o) noexcept : _p(o._p), _n(o._n), _cap(o._cap) { o._p = nullptr, o._n = o._cap = 0; }
+    PinnedArray(PinnedArray&& o) noexcept
+        : _p(o._p), _n(o._n), _cap(o._cap), _retired(std::move(o._retired))
+    {
+        o._p = nullptr, o._n = o._cap = 0;
+    }
     PinnedArray& operator=(PinnedArray&& o) noexcept
     {
         std::swap(_p, o._p);
         std::swap(_n, o._n);
         std::swap(_cap, o._cap);
+        std::swap(_retired, o._retired);
         return *this;
     }
     ~PinnedArray()
     {
         if (_p)
             wsg_host_free(_p);
+        for (void* q : _retired)
+            wsg_host_free(q);
     }
     T* data() noexcept { return _p; }
     const T* data() const noexcept { return _p; }
@@ -138,17 +148,19 @@ private:
         if (cap < 4096 / sizeof(T))
             cap = 4096 / sizeof(T);
         void* q = nullptr;
+        _retired.reserve(_retired.size() + 1);   // (before the allocation: nothing leaks if this throws)
         if (wsg_host_alloc(cap * sizeof(T), &q) != WSG_OK)
             throw std::bad_alloc();
         if (_n)
             std::memcpy(q, _p, _n * sizeof(T));
         if (_p)
-            wsg_host_free(_p);
+            _retired.push_back(_p);
         _p = static_cast<T*>(q);
         _cap = cap;
     }
     T* _p = nullptr;
     size_t _n = 0, _cap = 0;
+    std::vector<void*> _retired;   // earlier blocks, freed with the array
 };
 
 class WSReceiveBatch
@@ -168,6 +180,10 @@ public:
     void Clear(WebSocket& ws);
     //! Drop every queued frame of `ws` (call before destroying it)
     void Forget(WebSocket& ws);
+    //! Deliver every queued frame of `ws` (a connection leaving the batch):
+    //! flushes until none is queued and no other thread's flush is running.
+    //! From inside a callback of this thread's own flush it returns at once.
+    void Drain(WebSocket& ws);
     //! Unmask every queued frame on the GPU and deliver them in arrival
     //! order; returns the number of frames delivered.  A Flush() called from
     //! inside a callback returns 0 (its frames go with the next one).

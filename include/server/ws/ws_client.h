@@ -118,6 +118,14 @@ private:
     std::string _http_buf;   // upgrade response bytes until its header block is complete
     std::atomic<WSReceiveBatch*> _rx_batch{nullptr};   // swapped by SetReceiveBatch, read by the IO thread
     std::atomic<WSSendBatch*> _tx_batch{nullptr};
+    // held while a read (or a sync send) uses the batch it loaded; the swaps
+    // take it, so a batch swapped out has no user left and may be freed
+    QueueLock _rx_use, _tx_use;
+    // a receive batch this connection is leaving (SetReceiveBatch): until its
+    // queued frames of this connection are delivered, reads wait and a
+    // ResetBuffers queues its reset there (both under _rx_use)
+    bool _rx_draining = false;
+    WSReceiveBatch* _rx_prev = nullptr;
     void ResetBuffers();
     void RouteFrames(const void* buffer, size_t size);
     size_t SendFrame(uint8_t opcode, const void* buffer, size_t size, int status = 0,

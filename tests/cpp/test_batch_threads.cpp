@@ -1,13 +1,17 @@
 // test_batch_threads.cpp — the batches across threads (host only, no GPU):
 // one thread flushes (delivering frames to connections, handing frames to
 // transports) while another Forgets and destroys connections and
-// transports; and a connection destroyed on one thread while another
-// thread's BatchScope still holds frames it queued.  Built twice by
+// transports; a connection destroyed on one thread while another thread's
+// BatchScope still holds frames it queued; and a server's batched receive
+// and send switched on and off while IO threads read and send (a
+// read that had loaded the batch fed it after EnableBatchReceive(false) had
+// freed it).  Built twice by
 // tests/cpp/Makefile, under ThreadSanitizer and under AddressSanitizer, and
 // run by tests/test_sanitize.py.  Every frame carries key 0 (the server
 // direction, reference ws.cpp:206) or no mask, so no GPU pass runs: the batches
 // frame and hand out the bytes on the host exactly as they do around a GPU pass.
 #include "server/ws/ws_batch.h"
+#include "server/ws/ws_server.h"
 #include "server/ws/ws_session.h"
 #include "server/ws/ws_transport.h"
 
@@ -18,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <random>
 #include <thread>
@@ -329,8 +334,89 @@ static void test_cross_thread_destroy_in_callbacks(bool automatic)
     }
 }
 
+// A session that counts what it is delivered and checks it is alive.
+struct CountSession : WSSession {
+    using WSSession::WSSession;
+    uint64_t magic = kAlive;
+    std::atomic<uint64_t> bytes{0};
+    ~CountSession() override { magic = 0; }
+    void Ready() { Handshaked(false); }   // upgraded (server side: key 0, no GPU pass)
+
+protected:
+    void onWSReceived(const void* buffer, size_t size) override
+    {
+        CHECK(magic == kAlive);
+        bytes += size;
+    }
+};
+
+// IO threads feed their sessions' reads (RouteFrames) and send synchronously
+// (SendFrame flushes the send batch) while another thread switches the
+// server's batched receive and send on and off and a third flushes: no read
+// may use a batch after the switch freed it, and every frame of every read is
+// delivered exactly once (the frames a read put into a batch being switched
+// off are flushed by the switch, not lost).
+static void test_server_toggle_batches_while_reading()
+{
+    constexpr int kThreads = 4, kPerThread = 4, kReads = 3000, kFramesPerRead = 3, kLen = 24;
+    WSServer server;
+    std::vector<std::unique_ptr<Sink>> sinks;
+    std::vector<std::shared_ptr<CountSession>> sessions;
+    for (int i = 0; i < kThreads * kPerThread; ++i) {
+        sinks.push_back(std::make_unique<Sink>());
+        sessions.push_back(std::make_shared<CountSession>(*sinks.back()));
+        sessions.back()->Ready();
+        server.AddSession(sessions.back());
+    }
+    std::vector<uint8_t> read;
+    for (int k = 0; k < kFramesPerRead; ++k) {
+        const std::vector<uint8_t> f = unmasked_frame(kLen, uint8_t(0x40 + k));
+        read.insert(read.end(), f.begin(), f.end());
+    }
+    std::atomic<int> running{kThreads};
+    std::thread toggler([&] {
+        for (uint32_t i = 0; running.load() > 0; ++i) {
+            server.EnableBatchReceive(i & 1);
+            server.EnableBatchSend(i & 2);
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+        server.EnableBatchReceive(false);
+        server.EnableBatchSend(false);
+    });
+    std::thread flusher([&] {
+        while (running.load() > 0) {
+            server.FlushReceived();
+            server.FlushSend();
+            std::this_thread::yield();
+        }
+    });
+    std::vector<std::thread> io;
+    for (int t = 0; t < kThreads; ++t)
+        io.emplace_back([&, t] {
+            for (int r = 0; r < kReads; ++r) {
+                CountSession& s = *sessions[size_t(t * kPerThread + r % kPerThread)];
+                s.onReceived(read.data(), read.size());
+                if (r % 64 == 0)
+                    CHECK(s.SendBinary("sync", 4) == 6);   // 82 04 "sync"
+            }
+            --running;
+        });
+    for (auto& th : io)
+        th.join();
+    toggler.join();
+    flusher.join();
+    server.FlushReceived();
+    uint64_t got = 0;
+    for (auto& s : sessions)
+        got += s->bytes.load();
+    CHECK(got == uint64_t(kThreads) * kReads * kFramesPerRead * kLen);
+    for (auto& s : sessions)
+        server.RemoveSession(s);
+}
+
 int main()
 {
+    test_server_toggle_batches_while_reading();
     test_receive_forget_while_flushing();
     test_send_forget_while_flushing();
     test_session_destroyed_while_queued_elsewhere();

@@ -20,6 +20,16 @@ def test_cpp_ws_api():
     assert "0 failures" in r.stdout
 
 
+def test_concurrent_context_creation():
+    """Eight threads released together each create a context and decode one
+    host batch on it (tests/cpp/test_concurrent_create.cpp), in a fresh
+    process: every context made, every batch exact."""
+    exe = os.path.join(ROOT, "tests", "cpp", "_build", "test_concurrent_create")
+    assert os.path.exists(exe), "build tests/cpp first"
+    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+
+
 @pytest.mark.parametrize("mode,clients,threads", [("per_read", 1, 1), ("tick", 8, 1), ("per_read", 8, 2),
                                                   ("per_call", 1, 1)])
 def test_echo_c1_modes(mode, clients, threads):

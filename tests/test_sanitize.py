@@ -49,7 +49,9 @@ def test_sanitized_handshake():
 def test_batch_threads_tsan():
     """Forget / destroy a connection or transport on one thread
     while another flushes, and destroy a session whose frames sit in another
-    thread's BatchScope (tests/cpp/test_batch_threads.cpp, ThreadSanitizer)."""
+    thread's BatchScope; ADVICE r4: a server's batched receive and send
+    switched on and off while IO threads read and send, every frame delivered
+    once (tests/cpp/test_batch_threads.cpp, ThreadSanitizer)."""
     _make("threads")
     exe = os.path.join(CPP, "_build", "san", "test_batch_threads_tsan")
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1")
@@ -62,6 +64,19 @@ def test_batch_threads_tsan():
 def test_batch_threads_asan():
     _make("threads")
     _run(os.path.join(CPP, "_build", "san", "test_batch_threads_asan"))
+
+
+def test_concurrent_create_tsan():
+    """Eight threads create codec contexts at once (round 4's getenv crash in
+    wsg_create): under ThreadSanitizer, without a device every wsg_create
+    fails the same clean way (tests/cpp/test_concurrent_create.cpp; the GPU
+    run is tests/test_gpu_cpp_api.py::test_concurrent_context_creation)."""
+    _make("threads")
+    exe = os.path.join(CPP, "_build", "san", "test_concurrent_create_tsan")
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "WARNING: ThreadSanitizer" not in r.stderr
 
 
 def test_reference_api_compiles():
