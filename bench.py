@@ -51,7 +51,79 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip copy-ceiling and PCIe-inclusive legs")
     ap.add_argument("--no-configs", action="store_true", help="c2 at N=1: skip the C3/C4/C5 legs")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--dry-run", action="store_true",
+                    help="the rank launch and the line's shape only (gloo, no GPU work): tests of --gpus N")
     return ap.parse_args()
+
+
+XGMI_LINK_GBPS = 153.0   # one xGMI link, per direction (MI355X_MICROARCH.md)
+
+
+def root_ingress_expectation(world):
+    """GB/s the gather root can take in: one xGMI link from each other rank
+    (the node's GPUs are fully connected, 7 links each)."""
+    return round((world - 1) * XGMI_LINK_GBPS, 1) if world > 1 else None
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` (N > 1) outside a torch.distributed launch:
+    start one rank per GPU with torch.distributed.run as a child process (no
+    torch or GPU call in this one), pass its output through and exit with its
+    status.  Rank 0 prints the line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    r = subprocess.run(cmd, env=env)
+    sys.exit(r.returncode)
+
+
+def check_world(args):
+    """The ranks actually running must be the --gpus asked for: a mismatch
+    exits non-zero instead of reporting another N."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1:
+            launch_ranks(args)   # (does not return)
+        return
+    if int(env_world) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d: launch one rank per GPU asked for" % (env_world, args.gpus),
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+
+
+def dry_run(args):
+    """The launch path alone (gloo ranks, barrier, max over ranks): the line
+    with the fields the N-rank run fills, no GPU work."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True, "barrier_s": round(elapsed, 6),
+                          "root_ingress_expectation_GBps": root_ingress_expectation(world)}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
 
 
 def dist_setup(args):
@@ -884,7 +956,7 @@ def c5_rank_leg(world, rank, local, device, n_total=1 << 20, size=16384, chunk=1
         if rank == 0:
             moved = n_total * fsz - n_local * fsz
             res.update({"bytes_into_root": moved, "GBps_into_root": round(moved / (gat_ms * 1e-3) / 1e9, 1),
-                        "root_ingress_expectation_GBps": 1071 if world == 8 else None,
+                        "root_ingress_expectation_GBps": root_ingress_expectation(world),
                         "job_bytes": n_total * fsz})
             ok = bool(torch.equal(out_off, torch.arange(n_total + 1, dtype=torch.int64, device=device) * fsz))
             import oracle
@@ -1375,6 +1447,9 @@ def failed_checks(obj, path=""):
 
 def main():
     args = parse()
+    check_world(args)   # (--gpus N > 1 without a launch: starts the ranks and exits)
+    if args.dry_run:
+        return dry_run(args)
     failed = []
     import torch
 

@@ -318,10 +318,20 @@ WSSession::~WSSession()
     BatchScope::ForgetEverywhere(*this, _transport);
 }
 
-void WSSession::SetReceiveBatch(WSReceiveBatch* batch)
+void WSSession::SetReceiveBatch(WSReceiveBatch* batch) { SwapReceiveBatch(batch, true); }
+
+void WSSession::SwapReceiveBatch(WSReceiveBatch* batch, bool deliver)
 {
-    // swapped atomically (the IO thread reads it per read); the old batch
-    // delivers this connection's queued frames before its next read is taken
+    if (!deliver) {
+        WSReceiveBatch* old;
+        {
+            std::scoped_lock<QueueLock> use(_rx_use);   // (a read still feeding the old batch finishes first)
+            old = _rx_batch.exchange(batch, std::memory_order_acq_rel);
+        }
+        if (old && old != batch)
+            old->Forget(*this);
+        return;
+    }
     WSReceiveBatch* old;
     {
         std::scoped_lock<QueueLock> use(_rx_use);   // (a read still feeding the old batch finishes first)
@@ -565,7 +575,7 @@ void WSServer::RemoveSession(const std::shared_ptr<WSSession>& session)
     // batch's Forget may wait for a flush on another thread that is calling
     // into this session, and whose callbacks may take that lock
     if (detach) {
-        session->SetReceiveBatch(nullptr);
+        session->SwapReceiveBatch(nullptr, false);
         session->SetSendBatch(nullptr);
     }
 }

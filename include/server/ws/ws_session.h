@@ -103,6 +103,9 @@ protected:
 private:
     std::string _http_buf;   // upgrade request bytes until its header block is complete
     std::atomic<WSReceiveBatch*> _rx_batch{nullptr};   // swapped by SetReceiveBatch, read by the IO thread
+    // SetReceiveBatch; deliver = false (WSServer::RemoveSession): the frames
+    // it queued in the batch it leaves are dropped instead of delivered
+    void SwapReceiveBatch(WSReceiveBatch* batch, bool deliver);
     std::atomic<WSSendBatch*> _tx_batch{nullptr};
     // held while a read (or a sync send) uses the batch it loaded; the swaps
     // take it, so a batch swapped out has no user left and may be freed

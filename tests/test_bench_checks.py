@@ -40,3 +40,36 @@ def test_failed_checks_finds_misses_and_errors():
     assert "echo_c1.tcp_loopback.gpu_1c_1t.payload_ok=False" in got
     assert "lists[0].wire_ok=False" in got
     assert len(got) == 6
+
+
+def test_bench_gpus_n_starts_n_ranks():
+    """`python bench.py --gpus 2` (the driver's N=1 command shape with N=2)
+    starts two ranks itself (torch.distributed.run as a child process) and the
+    line reports n_gpus 2; --dry-run keeps it to the launch path (gloo, no
+    GPU work)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "1",
+                        "--warmup", "0"], capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["dry_run"] is True
+    assert line["root_ingress_expectation_GBps"] == 153.0
+
+
+def test_bench_world_mismatch_fails():
+    """A launch whose WORLD_SIZE is not --gpus exits non-zero instead of
+    reporting another N."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "WORLD_SIZE=3" in r.stderr
