@@ -55,14 +55,6 @@ struct wsg_ctx {
     // tools/c4_ab.py with graph-replayed launches; an empty kernel of that
     // grid is 1.65 us either way)
     int fan_wpb = 1;
-    // fan-out grid path (k_fanout_tables + k_fanout_grid) for calls of at
-    // least this many messages of one geometry; 0: never ($WSG_FAN_GRID, an
-    // A/B knob, off: 16 x C4 in 203 us against the period kernel's 122, its
-    // lanes' two dependent L2 round trips per 16-B store,
-    // profiles/r4/fan_grid_ab.log)
-    uint32_t fan_grid_min = 0;
-    void* d_fan_tab = nullptr;   // its chunk-template table
-    uint64_t fan_tab_bytes = 0;
     uint64_t small_avg = wsg::SMALL_AVG;   // batch encode: k_encode_small when wire_cap <= n * small_avg
     unsigned long long* d_err = nullptr;        // latch of the caller-visible async entry points (wsg_sync)
     unsigned long long* d_err_host = nullptr;   // latch of the host-staged pipelines (their own status)
@@ -813,7 +805,6 @@ int wsg_destroy(wsg_ctx* c)
     }
     (void)hipFree(c->d_err);
     (void)hipFree(c->d_err_host);
-    (void)hipFree(c->d_fan_tab);
     free_enc(c->enc);
     (void)hipFree(c->d_stage);
     (void)hipFree(c->d_fs);
@@ -1048,22 +1039,6 @@ int fanout_many(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, const uint6
                 g.dst[q] = wire_off[members[at + q]];
             }
             hipError_t perr = hipSuccess;
-            if (c->fan_grid_min && cnt >= c->fan_grid_min) {
-                // many messages: the grid path, its table grown as needed
-                const uint64_t need = wsg::fanout_grid_table_bytes(fsize, k, cnt);
-                if (need && need > c->fan_tab_bytes) {
-                    (void)hipFree(c->d_fan_tab);
-                    c->d_fan_tab = nullptr;
-                    c->fan_tab_bytes = 0;
-                    if (hipMalloc(&c->d_fan_tab, need) == hipSuccess)
-                        c->fan_tab_bytes = need;
-                }
-                if (need && wsg::launch_fanout_grid(s, d_payload, len[i], d_keys, k, opcode[i], mask ? 1u : 0u, fsize,
-                                                    d_wire, g, cnt, c->d_fan_tab, c->fan_tab_bytes, &perr)) {
-                    WSG_HIP(perr);
-                    continue;
-                }
-            }
             if (wsg::launch_fanout_period(s, c->num_cus, c->fan_waves_per_cu, c->fan_wpb, d_payload, len[i], d_keys, k, opcode[i],
                                           mask ? 1u : 0u, fsize, d_wire, g, cnt, &perr)) {
                 WSG_HIP(perr);

@@ -83,13 +83,6 @@ struct FanMsgs {
 bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, int wpb, const uint8_t* payload, uint64_t len,
                           const uint32_t* keys, uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize,
                           uint8_t* wire, const FanMsgs& msgs, uint32_t nmsgs, hipError_t* err);
-// Grid path of the period formula (many messages): a table kernel then one
-// lane per chunk; `table` of fanout_grid_table_bytes() bytes (0: not
-// eligible).  false: not taken (the caller uses the period / flat paths).
-uint64_t fanout_grid_table_bytes(uint64_t fsize, uint32_t k, uint32_t nmsgs);
-bool launch_fanout_grid(hipStream_t s, const uint8_t* payload, uint64_t len, const uint32_t* keys, uint32_t k,
-                        uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire, const FanMsgs& msgs,
-                        uint32_t nmsgs, void* table, uint64_t table_bytes, hipError_t* err);
 hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64_t len, const uint32_t* keys,
                          uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire);
 hipError_t launch_xor(hipStream_t s, int grid, const uint8_t* src, uint8_t* dst, uint64_t len, uint32_t key,

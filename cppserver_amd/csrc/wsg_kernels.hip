@@ -74,17 +74,11 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_FAN_PERIOD
 #define WSG_FAN_PERIOD 1   // fan-out: period path (k_fanout_period) where the frame size allows; 0 = flat kernel only
 #endif
-#ifndef WSG_ENC_PRO
-#define WSG_ENC_PRO 0   // k_encode_mask: 1 = the prologue's independent loads in one round (A/B, tools/tune_enc.py: C3 -0.5 %, C5 share +2 %; not kept)
-#endif
 #ifndef WSG_FAN_PRO
 #define WSG_FAN_PRO 1   // fan-out period path prologue (A/B, tools/c4_ab.py): 1 all kernel arguments loaded in one round, 2 both payload windows issued together branch-free, 4 early exit past the last row
 #endif
 #ifndef WSG_FAN_KSEL
 #define WSG_FAN_KSEL 2   // fan-out period path: a pass's keys by ds_bpermute one pass ahead (2: C4 8.32 vs 8.40 us) or in the pass (0); v_readlane + per-lane selects measured 8.6 us (round 3)
-#endif
-#ifndef WSG_FAN_SLIDE
-#define WSG_FAN_SLIDE 0   // fan-out period path: keys in sliding windows (any passes per wave; A/B)
 #endif
 #ifndef WSG_FAN_UNROLL
 #define WSG_FAN_UNROLL 1   // fan-out period path: passes per loop iteration (A/B)
@@ -1254,33 +1248,9 @@ __global__ __launch_bounds__(BLOCK) void k_encode_mask(const uint8_t* __restrict
 {
     const uint32_t waves = gridDim.x * (BLOCK / 64);
     uint32_t q = q_begin + blockIdx.x * (BLOCK / 64) + wave_id();
-    uint32_t pieces, f_first = 0, f_second = 0;
-    if (WSG_ENC_PRO) {
-        // The prologue's independent loads in one round: the batch's end and
-        // piece count, and this wave's first two piece -> frame entries (the
-        // map holds q_end entries; entries past the batch's pieces are never
-        // used).  Left to the compiler these came in seven dependent scalar
-        // rounds (kernel arguments among them) before a piece's first data
-        // load, several us per wave for 4 KiB of work.
-        // (no asm barrier before these loads: the compiler then treats
-        // memory as possibly written and turns them into vector loads)
-        const uint64_t end = wire_off[n];
-        const uint32_t pall = piece_start[n];
-        f_first = piece_frame[min(q, q_end - 1)];           // (clamped, not branched: one round)
-        f_second = piece_frame[min(q + waves, q_end - 1)];
-        // identity asm (no memory effect): the four values exist here, so
-        // the compiler cannot sink their loads past the exits below
-        uint64_t e = end;
-        uint32_t pa = pall;
-        asm("" : "+s"(e), "+s"(pa), "+s"(f_first), "+s"(f_second));
-        if (e > wire_cap)
-            return;   // capacity error latched by k_encode_finalize
-        pieces = min(pa, q_end);     // this launch's pieces: [q_begin, min(all pieces, q_end))
-    } else {
-        if (wire_off[n] > wire_cap)
-            return;   // capacity error latched by k_encode_finalize
-        pieces = min(piece_start[n], q_end);
-    }
+    if (wire_off[n] > wire_cap)
+        return;   // capacity error latched by k_encode_finalize
+    const uint32_t pieces = min(piece_start[n], q_end);   // this launch's pieces: [q_begin, min(all pieces, q_end))
     // Software pipeline over the wave's pieces: while piece q streams, the
     // descriptor of piece q + W (frame index already known) and the frame
     // index of piece q + 2W are in flight, so the dependent metadata loads
@@ -1293,8 +1263,8 @@ __global__ __launch_bounds__(BLOCK) void k_encode_mask(const uint8_t* __restrict
     auto meta = [&](uint32_t i) { return Meta{load_desc(desc + i), wire_off[i], piece_start[i]}; };
     if (q >= pieces)
         return;
-    Meta cur = meta(WSG_ENC_PRO ? f_first : piece_frame[q]);
-    uint32_t i_next = (q + waves < pieces) ? (WSG_ENC_PRO ? f_second : piece_frame[q + waves]) : 0;
+    Meta cur = meta(piece_frame[q]);
+    uint32_t i_next = (q + waves < pieces) ? piece_frame[q + waves] : 0;
     for (;;) {
         Piece<WSG_ENC_NT_SRC != 0> pc;
         pc.load(make_rec(cur.off, payload + cur.d.src_off, cur.d.len, cur.d.key, cur.d.status, cur.d.opcode,
@@ -2182,28 +2152,14 @@ __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restric
     // payload loads, so the two arrive together: the kernel is short (41 MB
     // at C4), and a second dependent memory round trip before the first
     // store was a visible share of it
-    // WSG_FAN_SLIDE: the keys come in windows of PW passes (kv: the current
-    // window, kv_nx: the next, loaded a window ahead), so a wave may make any
-    // number of passes (fewer, longer-lived waves: the write stream of
-    // tools/membench.hip's row pattern at 4 waves/CU)
-    constexpr uint32_t PW = 64 * WSG_FAN_KV / KW;   // passes per key window
-    auto load_window = [&](uint32_t w0, uint32_t (&dst)[WSG_FAN_KV]) {
+    uint32_t kv[WSG_FAN_KV];
 #pragma unroll
-        for (int h = 0; h < WSG_FAN_KV; ++h) {
-            const uint32_t s = uint32_t(h) * 64 + lane;
-            const uint64_t it = uint64_t(w0) + s / KW;
-            const uint64_t idx = uint64_t(P) * (m0 + it * dm) + (s % KW);
-            dst[h] = (WSG_DIAG_FAN & 32) ? uint32_t(idx) : (row0 + it * rstep < chunks && idx < k) ? keys[idx] : 0u;
-        }
-    };
-    uint32_t kv[WSG_FAN_KV], kv_nx[WSG_FAN_KV];
-    load_window(0, kv);
-    if (WSG_FAN_SLIDE)
-        load_window(PW, kv_nx);
-    else
-        for (int h = 0; h < WSG_FAN_KV; ++h)
-            kv_nx[h] = 0;
-    uint32_t w0 = 0;   // first pass of the window in kv
+    for (int h = 0; h < WSG_FAN_KV; ++h) {
+        const uint32_t s = uint32_t(h) * 64 + lane;
+        const uint64_t it = s / KW;
+        const uint64_t idx = uint64_t(P) * (m0 + it * dm) + (s % KW);
+        kv[h] = (WSG_DIAG_FAN & 32) ? uint32_t(idx) : (row0 + it * rstep < chunks && idx < k) ? keys[idx] : 0u;
+    }
 
     // template of chunk j: its frame-a bytes, and the next frame's from byte
     // `split` on (the first 16 bytes of a frame: the same for every lane)
@@ -2264,19 +2220,11 @@ __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restric
     // The keys of pass `it` for this lane: frame a's (slot ia) and, where a
     // frame starts inside the lane's chunk, frame b's (slot ia + 1).
     auto pass_keys = [&](uint32_t it, uint32_t& ka, uint32_t& kb, bool want_b) {
-        uint32_t slot = (it - w0) * KW;                     // wave-uniform; KW divides 64
+        const uint32_t slot = it * KW;                      // wave-uniform; KW divides 64
         uint32_t kreg = kv[0];
-        if (WSG_FAN_SLIDE && slot >= 64 * WSG_FAN_KV) {    // the next window's (one pass ahead)
-            slot -= 64 * WSG_FAN_KV;
-            kreg = kv_nx[0];
 #pragma unroll
-            for (int h = 1; h < WSG_FAN_KV; ++h)
-                kreg = (slot >> 6) == uint32_t(h) ? kv_nx[h] : kreg;
-        } else {
-#pragma unroll
-            for (int h = 1; h < WSG_FAN_KV; ++h)
-                kreg = (slot >> 6) == uint32_t(h) ? kv[h] : kreg;
-        }
+        for (int h = 1; h < WSG_FAN_KV; ++h)
+            kreg = (slot >> 6) == uint32_t(h) ? kv[h] : kreg;
         const uint32_t sb = (slot & 63) * 4;
         ka = __builtin_amdgcn_ds_bpermute(int(addr + sb), int(kreg));
         kb = want_b ? __builtin_amdgcn_ds_bpermute(int(addr + sb + 4), int(kreg)) : 0u;
@@ -2313,13 +2261,6 @@ __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restric
 #pragma unroll WSG_FAN_UNROLL
         for (uint32_t it = 0; it < n_full; ++it) {
             const v4u w = word(it);
-            if (WSG_FAN_SLIDE && it + 1 - w0 == PW) {   // (wave-uniform) the next window takes over
-#pragma unroll
-                for (int h = 0; h < WSG_FAN_KV; ++h)
-                    kv[h] = kv_nx[h];
-                w0 += PW;
-                load_window(w0 + PW, kv_nx);
-            }
             if ((WSG_DIAG_FAN & 64) && (w[0] & w[1] & w[2] & w[3]) != 0xA5C3E1F7u) {
                 // diagnostic: the computation without its stores
             } else if (WSG_FAN_SC1) {
@@ -2445,167 +2386,6 @@ hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64
     return hipGetLastError();
 }
 
-// ---- fan-out, grid path (many messages in one call) ------------------------
-// The same chunk formula as the period path, laid out as the plain fill the
-// write stream runs fastest as (tools/membench.hip: one 16-B store per lane
-// and a grid over every chunk, 98 us for 657 MB against 106-117 us for the
-// period kernel's 1 KiB rows per wave per pass): a small first kernel
-// writes every message's G chunk templates (T, MA, MB, the key rotations,
-// the frame of the group) into a table, and the second gives every chunk of
-// every message one lane — its group from one float multiply, its template
-// and its one or two keys from L2, one nontemporal store.
-struct FanEntry {
-    v4u t, ma, mb;
-    uint32_t w[4];   // w[0] = frame of the group (qa) | sa << 8 | sbr << 16 | has_b << 24
-};
-static_assert(sizeof(FanEntry) == 64, "fan-out table entry");
-
-template <int P>
-__global__ __launch_bounds__(256) void k_fanout_tables(const uint8_t* __restrict__ payload0, uint64_t len,
-                                                       uint8_t opcode, uint32_t mask, uint64_t fsize, uint32_t G,
-                                                       const FanMsgs msgs, v4u hp0, FanEntry* __restrict__ tab)
-{
-    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= G)
-        return;
-    const uint8_t* __restrict__ payload = payload0 + msgs.src[blockIdx.y];
-    FanGeom f;   // as k_fanout_period
-    f.g = send_geom(opcode, mask != 0, len, 0);
-    f.data0 = f.g.hdr + f.g.prefix;
-    f.kpos = f.g.hdr - (mask ? 4u : 0u);
-    f.mask = mask != 0;
-    f.hp0 = hp0;
-    const uint64_t o = uint64_t(j) * CHUNK;
-    uint32_t qa = 0;
-#pragma unroll
-    for (int q = 1; q < P; ++q)
-        qa += o >= uint64_t(q) * fsize ? 1u : 0u;
-    const uint64_t r = o - uint64_t(qa) * fsize;
-    v4u t, ma, mb = {0, 0, 0, 0};
-    fan_tm(payload, len, f, fsize, r, t, ma);
-    const uint64_t split = fsize - r;
-    uint32_t hb = 0;
-    if (split < CHUNK) {
-        v4u t0, m0v;
-        fan_tm(payload, len, f, fsize, 0, t0, m0v);
-        t |= shl_bytes(t0, split);
-        mb = shl_bytes(m0v, split);
-        hb = 1;
-    }
-    const uint32_t pa = uint32_t(r - f.g.hdr), pb = uint32_t(0u - uint32_t(split) - f.g.hdr);
-    FanEntry e;
-    e.t = t;
-    e.ma = ma;
-    e.mb = mb;
-    e.w[0] = qa | ((8u * (pa & 3u)) << 8) | ((8u * (pb & 3u)) << 16) | (hb << 24);
-    e.w[1] = e.w[2] = e.w[3] = 0;
-    tab[size_t(blockIdx.y) * G + j] = e;
-}
-
-template <int P>
-__global__ __launch_bounds__(256) void k_fanout_grid(const uint32_t* __restrict__ keys, uint32_t k, uint32_t G,
-                                                     float inv_g, uint32_t chunks, uint64_t total,
-                                                     uint8_t* __restrict__ wire0, const FanMsgs msgs,
-                                                     const FanEntry* __restrict__ tab)
-{
-    const uint32_t c = blockIdx.x * 256 + threadIdx.x;   // chunk of message blockIdx.y (host: chunks < 2^24)
-    if (c >= chunks)
-        return;
-    int32_t g = int32_t(float(c) * inv_g);               // its group, exact after one correction
-    int32_t j = int32_t(c) - g * int32_t(G);
-    if (j < 0) {
-        --g;
-        j += int32_t(G);
-    } else if (j >= int32_t(G)) {
-        ++g;
-        j -= int32_t(G);
-    }
-    const FanEntry* __restrict__ e = tab + size_t(blockIdx.y) * G + uint32_t(j);
-    const uint32_t w = e->w[0];
-    const uint32_t ia = uint32_t(g) * P + (w & 0xFFu);
-    const bool hb = (w >> 24) != 0;
-    const uint32_t ka = ia < k ? keys[ia] : 0u;
-    const uint32_t kb = (hb && ia + 1 < k) ? keys[ia + 1] : 0u;
-    const uint32_t ra = __builtin_amdgcn_alignbit(ka, ka, (w >> 8) & 0xFFu);
-    const uint32_t rb = __builtin_amdgcn_alignbit(kb, kb, (w >> 16) & 0xFFu);
-    const v4u out = e->t ^ (e->ma & v4u{ra, ra, ra, ra}) ^ (e->mb & v4u{rb, rb, rb, rb});
-    uint8_t* __restrict__ wire = wire0 + msgs.dst[blockIdx.y];
-    if (c + 1 < chunks || (total & (CHUNK - 1)) == 0) {
-        st16nt(wire + uint64_t(c) * CHUNK, out);
-    } else {
-#pragma unroll 1
-        for (uint32_t b = 0; b < uint32_t(total & (CHUNK - 1)); ++b)
-            wire[uint64_t(c) * CHUNK + b] = uint8_t(lane_byte(out, b));
-    }
-}
-
-// Grid path for nmsgs messages of one geometry when the frame size allows
-// the period formula and each message's chunks fit 2^24; `table` holds at
-// least fanout_grid_table_bytes(...) bytes.  false: not taken.
-bool fanout_grid_shape(uint64_t fsize, uint32_t k, uint32_t& P, uint32_t& G)
-{
-    if (fsize % 4 != 0)
-        return false;
-    uint64_t g16 = 16;
-    while (fsize % g16)
-        g16 >>= 1;
-    P = uint32_t(16 / g16);
-    const uint64_t g = uint64_t(P) * fsize / CHUNK;
-    const uint64_t chunks = (fsize * k + CHUNK - 1) / CHUNK;
-    if (g < 1 || g > (1u << 20) || chunks >= (uint64_t(1) << 24) || uint64_t(k) * P >= (uint64_t(1) << 31))
-        return false;
-    G = uint32_t(g);
-    return true;
-}
-
-uint64_t fanout_grid_table_bytes(uint64_t fsize, uint32_t k, uint32_t nmsgs)
-{
-    uint32_t P, G;
-    if (!fanout_grid_shape(fsize, k, P, G))
-        return 0;
-    return uint64_t(nmsgs) * G * sizeof(FanEntry);
-}
-
-bool launch_fanout_grid(hipStream_t s, const uint8_t* payload, uint64_t len, const uint32_t* keys, uint32_t k,
-                        uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire, const FanMsgs& msgs,
-                        uint32_t nmsgs, void* table, uint64_t table_bytes, hipError_t* err)
-{
-    uint32_t P, G;
-    if (nmsgs == 0 || nmsgs > uint32_t(FAN_MSGS) || !fanout_grid_shape(fsize, k, P, G) ||
-        table_bytes < uint64_t(nmsgs) * G * sizeof(FanEntry) || !table)
-        return false;
-    for (uint32_t y = 0; y < nmsgs; ++y)
-        if (((reinterpret_cast<uintptr_t>(wire) + msgs.dst[y]) & (CHUNK - 1)) != 0)
-            return false;   // (16-B stores at each message's start)
-    const uint64_t total = fsize * k;
-    const uint32_t chunks = uint32_t((total + CHUNK - 1) / CHUNK);
-    const SendGeom sg = send_geom(opcode, mask != 0, len, 0);
-    const uint32_t kpos = sg.hdr - (mask ? 4u : 0u);
-    uint32_t hw[4] = {0, 0, 0, 0};
-    for (uint32_t r = 0; r < kpos; ++r)
-        hw[r / 4] |= uint32_t(header_byte(opcode, mask != 0, sg.body, 0, r)) << (8 * (r % 4));
-    const v4u hp0 = v4u{hw[0], hw[1], hw[2], hw[3]};
-    FanEntry* tab = static_cast<FanEntry*>(table);
-    const dim3 tg((G + 255) / 256, nmsgs), sg2((chunks + 255) / 256, nmsgs);
-    const float inv_g = 1.0f / float(G);
-    switch (P) {
-    case 1:
-        k_fanout_tables<1><<<tg, 256, 0, s>>>(payload, len, opcode, mask, fsize, G, msgs, hp0, tab);
-        k_fanout_grid<1><<<sg2, 256, 0, s>>>(keys, k, G, inv_g, chunks, total, wire, msgs, tab);
-        break;
-    case 2:
-        k_fanout_tables<2><<<tg, 256, 0, s>>>(payload, len, opcode, mask, fsize, G, msgs, hp0, tab);
-        k_fanout_grid<2><<<sg2, 256, 0, s>>>(keys, k, G, inv_g, chunks, total, wire, msgs, tab);
-        break;
-    default:
-        k_fanout_tables<4><<<tg, 256, 0, s>>>(payload, len, opcode, mask, fsize, G, msgs, hp0, tab);
-        k_fanout_grid<4><<<sg2, 256, 0, s>>>(keys, k, G, inv_g, chunks, total, wire, msgs, tab);
-        break;
-    }
-    *err = hipGetLastError();
-    return true;
-}
-
 // Period path (k_fanout_period) when the frame size allows it; returns false
 // to leave the batch to k_fanout_flat.  Wave count W = Q * s with W * 64 a
 // multiple of G (Q = G / gcd(G, 64)), about `waves` of them, and few enough
@@ -2636,8 +2416,7 @@ bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, int wpb, con
     const uint64_t rows = (chunks + 63) / 64;
     uint64_t mult = std::max<uint64_t>(1, (uint64_t(cus) * waves_per_cu + Q / 2) / Q);
     mult = std::min(mult, (rows + Q - 1) / Q);                                                 // no idle waves
-    if (!WSG_FAN_SLIDE)   // every pass's keys in one load per lane
-        mult = std::max(mult, (chunks + Q * 64 * max_passes - 1) / (Q * 64 * max_passes));
+    mult = std::max(mult, (chunks + Q * 64 * max_passes - 1) / (Q * 64 * max_passes));   // every pass's keys in one load per lane
     const uint64_t W = Q * mult;
     if (W > (1u << 22))
         return false;

@@ -461,14 +461,11 @@ def test_fanout_many_vs_oracle(codec, case):
     (8190, 130, 0x89),   # ping with the status prefix: F = 8200, P = 2
     (65538, 40, 0x82),   # 8-byte length form: F = 65552
 ])
-def test_fanout_grid_path(length, k, opcode):
-    """With $WSG_FAN_GRID=2 (an A/B knob, off by default), calls of several
-    messages of one geometry take the grid path (k_fanout_tables +
-    k_fanout_grid: one lane per chunk): every message's
-    frames equal oracle.fanout_encode's, as the period path's
-    ($WSG_FAN_GRID=0) do, masked and unmasked."""
-    import os
-
+def test_fanout_many_geometries(length, k, opcode):
+    """Several messages of one geometry in one call (wsg_fanout_encode_many)
+    for every group period of the period kernel (P = 1, 2, 4, partial last
+    chunk) and frame sizes it leaves to the flat kernel: every message's frames
+    equal oracle.fanout_encode's, masked and unmasked."""
     rng = np.random.default_rng(length * 31 + k)
     m = 3
     keys = rng.integers(0, 2**32, k, dtype=np.uint64).astype(np.uint32)
@@ -477,40 +474,18 @@ def test_fanout_grid_path(length, k, opcode):
     src = np.zeros(m, np.uint64)
     src[1:] = np.cumsum(lens[:-1] + 5)            # unaligned message starts
     arena = wl.random_bytes(rng, int(src[-1] + lens[-1] + 16))
-    old = os.environ.get("WSG_FAN_GRID")
-    try:
-        os.environ["WSG_FAN_GRID"] = "0"
-        period = ca.Codec(0)
-    finally:
-        if old is None:
-            os.environ.pop("WSG_FAN_GRID", None)
-        else:
-            os.environ["WSG_FAN_GRID"] = old
-    try:
-        os.environ["WSG_FAN_GRID"] = "2"
-        grid = ca.Codec(0)
-    finally:
-        if old is None:
-            os.environ.pop("WSG_FAN_GRID", None)
-        else:
-            os.environ["WSG_FAN_GRID"] = old
+    c = ca.Codec(0)
     try:
         for mask in (True, False):
-            outs = []
-            for c in (grid, period):
-                wire_t, off = c.fanout_many(dev(arena), src, lens, ops, dev(keys.view(np.int32)), mask=mask)
-                c.sync()
-                outs.append((wire_t.cpu().numpy(), off))
-            (got, off), (per, off_p) = outs
-            assert np.array_equal(off, off_p)
-            for i in range(m):   # (the padding between messages is not written by either path)
+            wire_t, off = c.fanout_many(dev(arena), src, lens, ops, dev(keys.view(np.int32)), mask=mask)
+            c.sync()
+            got = wire_t.cpu().numpy()
+            for i in range(m):
                 ref = oracle.fanout_encode(arena[int(src[i]): int(src[i]) + length], keys, opcode, mask)
                 a = int(off[i])
                 assert np.array_equal(got[a: a + len(ref)], ref), (i, mask)
-                assert np.array_equal(per[a: a + len(ref)], ref), (i, mask)
     finally:
-        grid.close()
-        period.close()
+        c.close()
 
 
 def test_fanout_many_capacity(codec):

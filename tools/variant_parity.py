@@ -72,7 +72,7 @@ def main():
     seeds = int(sys.argv[2]) if len(sys.argv) > 2 else 300
     c = ca.Codec(0, lib_path=os.path.join(ROOT, "cppserver_amd", "_build", "var", name, "libwsg.so"))
     if "--fanout" in sys.argv:
-        print(json.dumps(dict(variant=name, **fanout_parity(c, seeds, os.environ.get("WSG_FAN_WAVES_PER_CU")))),
+        print(json.dumps(dict(variant=name, **fanout_parity(c, seeds, None))),
               flush=True)
         return
     bad = []
