@@ -83,6 +83,13 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_FAN_UNROLL
 #define WSG_FAN_UNROLL 1   // fan-out period path: passes per loop iteration (A/B)
 #endif
+#ifndef WSG_FAN_CAP
+// fan-out period path, many messages per launch: at most this many (one-wave)
+// workgroups per CU, by a dynamic LDS reserve the kernel does not use; the
+// register-limited 7 per SIMD wrote 16 x C4 in 121 us, 4 per CU in 112-114
+// (the runtime's fill of the same bytes: 97 us; profiles/r5/fan_cap_ab.log)
+#define WSG_FAN_CAP 4
+#endif
 #ifndef WSG_FAN_KV
 #define WSG_FAN_KV 2   // fan-out period path: key registers per lane (64 pass-window slots each)
 #endif
@@ -2433,19 +2440,23 @@ bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, int wpb, con
     for (uint32_t r = 0; r < kpos; ++r)
         hw[r / 4] |= uint32_t(header_byte(opcode, mask != 0, sg.body, 0, r)) << (8 * (r % 4));
     const v4u hp0 = v4u{hw[0], hw[1], hw[2], hw[3]};
+    // (WSG_FAN_CAP: LDS reserved per workgroup only to bound the workgroups
+    // resident per CU; the kernel uses none)
+    // (many messages only: one message's waves are all resident anyway)
+    const uint32_t lds = WSG_FAN_CAP && nmsgs > 1 ? uint32_t((160u << 10) / WSG_FAN_CAP) & ~255u : 0u;
     switch (P) {
     case 1:
-        k_fanout_period<1><<<dim3(blocks, nmsgs), 64 * uint32_t(wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize,
+        k_fanout_period<1><<<dim3(blocks, nmsgs), 64 * uint32_t(wpb), lds, s>>>(payload, len, keys, k, opcode, mask, fsize,
                                                                              uint32_t(G), dm, wire, msgs, hp0, uint32_t(W),
                                                                              uint32_t(wpb));
         break;
     case 2:
-        k_fanout_period<2><<<dim3(blocks, nmsgs), 64 * uint32_t(wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize,
+        k_fanout_period<2><<<dim3(blocks, nmsgs), 64 * uint32_t(wpb), lds, s>>>(payload, len, keys, k, opcode, mask, fsize,
                                                                              uint32_t(G), dm, wire, msgs, hp0, uint32_t(W),
                                                                              uint32_t(wpb));
         break;
     default:
-        k_fanout_period<4><<<dim3(blocks, nmsgs), 64 * uint32_t(wpb), 0, s>>>(payload, len, keys, k, opcode, mask, fsize,
+        k_fanout_period<4><<<dim3(blocks, nmsgs), 64 * uint32_t(wpb), lds, s>>>(payload, len, keys, k, opcode, mask, fsize,
                                                                              uint32_t(G), dm, wire, msgs, hp0, uint32_t(W),
                                                                              uint32_t(wpb));
         break;

@@ -377,6 +377,24 @@ __global__ __launch_bounds__(64 * RW) void k_rows(uint8_t* __restrict__ dst, uin
     }
 }
 
+
+// Write runs: wave w of the grid (4-wave blocks) writes U consecutive 1 KiB
+// rows [w U, w U + U), one 16-B store per lane per row (CONTIG = 1), or the
+// block's 4U rows interleaved over its waves (CONTIG = 0: wave q of the
+// block writes rows u * 4 + q, the fill's U-per-lane shape); every wave
+// stores U times and leaves (a dense write front in grid order).
+template <int U, int CONTIG>
+__global__ __launch_bounds__(256) void k_wrun(uint8_t* __restrict__ dst, uint64_t rows, uint32_t key)
+{
+    const uint32_t q = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t r = CONTIG ? (uint64_t(blockIdx.x) * 4 + q) * U + u : uint64_t(blockIdx.x) * 4 * U + u * 4 + q;
+        if (r < rows)
+            __builtin_nontemporal_store(u32x4{uint32_t(r), key, lane, key}, reinterpret_cast<u32x4*>(dst + r * 1024) + lane);
+    }
+}
+
 // LDS-DMA streaming copy-with-XOR: each wave owns pieces of U KiB (dealt
 // round-robin over all waves of a resident grid) and loads them with
 // global_load_lds_dwordx4 into a D-deep per-wave ring in LDS, so D-1 pieces
@@ -650,6 +668,30 @@ int main(int argc, char** argv)
                     double ms = time_kernel([&](int) { k_empty<<<blocks, threads>>>(d, 1u); });
                     printf("empty blocks=%5d threads=%3d %8.2f us\n", blocks, threads, ms * 1e3);
                 }
+        CK(hipFree(d));
+        return 0;
+    }
+    if (argc > 2 && std::string(argv[2]) == "wrun") {
+        // write runs of U rows per wave (k_wrun), contiguous vs interleaved,
+        // against the fill's one store per lane, on argv[1] MiB (626 =
+        // ws_multicast's 16-message tick; 0 = one C4, 41,040,000 B)
+        const uint64_t bytes41 = (mib ? n16 * 16 : 41040000ull) / 1024 * 1024;
+        uint8_t* d;
+        CK(hipMalloc(&d, 2 * bytes41 + 4096));
+        const uint64_t rows = bytes41 / 1024;
+#define WR(U, C)                                                                                                        \
+    {                                                                                                                   \
+        const int blocks = int((rows + 4 * U - 1) / (4 * U));                                                           \
+        double ms = time_kernel([&](int i) { k_wrun<U, C><<<blocks, 256>>>(d + (i & 1) * bytes41, rows, 7u); });       \
+        printf("wrun U=%2d contig=%d blocks=%7d  %8.2f us  %7.1f GB/s\n", U, C, blocks, ms * 1e3,                       \
+               bytes41 / (ms * 1e-3) / 1e9);                                                                            \
+    }
+        for (int rep = 0; rep < 2; ++rep) {
+            WR(1, 1) WR(2, 1) WR(4, 1) WR(8, 1) WR(16, 1) WR(2, 0) WR(4, 0) WR(8, 0)
+            double ms = time_kernel([&](int i) { CK(hipMemsetAsync(d + (i & 1) * bytes41, i, bytes41)); });
+            printf("hipMemsetAsync          %8.2f us  %7.1f GB/s\n", ms * 1e3, bytes41 / (ms * 1e-3) / 1e9);
+        }
+#undef WR
         CK(hipFree(d));
         return 0;
     }
