@@ -43,6 +43,7 @@ struct wsg_ctx {
     uint64_t enc_launch_pieces = 0;   // k_encode_mask: pieces per launch (0: all in one)
     uint64_t xor_direct_max = 64 << 10;   // per-call XOR off the lane: kernel on the pinned stage up to this size
     uint64_t seg_bytes = 32ull << 20;     // staged host pipelines: segment of about this many wire bytes ($WSG_STAGE_MB)
+    bool multi_share = false;             // multi-context splits keep several contexts of one device ($WSG_HOST_MULTI_SHARE)
     // host batches up to this many wire bytes whose buffers are page-locked:
     // the kernels read and write them in place (one launch sequence and one
     // synchronize, no staging copies); $WSG_HOST_DIRECT_MAX
@@ -255,6 +256,7 @@ int drain_timing(wsg_ctx* c)
 } // namespace
 
 int wsg::ctx_device(const wsg_ctx* c) { return c ? c->device : 0; }
+bool wsg::ctx_multi_share(const wsg_ctx* c) { return c && c->multi_share; }
 
 namespace {
 
@@ -706,6 +708,7 @@ struct Knobs {
     uint64_t host_direct_max = 4 << 20;            // $WSG_HOST_DIRECT_MAX: host batches read in place up to this
     uint64_t seg_bytes = 32ull << 20;              // $WSG_STAGE_MB: segment of the staged host pipelines
     int enc_blocks_per_cu = 0;                     // $WSG_ENC_BLOCKS_PER_CU: k_encode_mask grid cap (0: default)
+    bool multi_share = false;                      // $WSG_HOST_MULTI_SHARE=1: multi-context splits keep contexts of one device
     uint64_t enc_launch_pieces = 0;                // $WSG_ENC_LAUNCH_PIECES: pieces per k_encode_mask launch
 };
 
@@ -733,6 +736,8 @@ Knobs read_knobs()
     }
     if (const char* e = wsg::envp("WSG_ENC_LAUNCH_PIECES"))     // (tests: split launches)
         k.enc_launch_pieces = std::strtoull(e, nullptr, 10);
+    if (const char* e = wsg::envp("WSG_HOST_MULTI_SHARE"))      // (one-GPU tests of the multi-device split)
+        k.multi_share = *e == '1';
     return k;
 }
 
@@ -784,6 +789,7 @@ int wsg_create(int device, wsg_ctx** out)
     if (k.enc_blocks_per_cu)
         c->enc_blocks_per_cu = k.enc_blocks_per_cu;
     c->enc_launch_pieces = k.enc_launch_pieces;
+    c->multi_share = k.multi_share;
     *out = c;
     return WSG_OK;
 }

@@ -179,5 +179,7 @@ hipError_t launch_lane(hipStream_t s, LaneBell* bell, uint32_t workgroups, uint6
 
 // HIP device a context is bound to (wsg_capi.hip)
 int ctx_device(const wsg_ctx* c);
+// $WSG_HOST_MULTI_SHARE as the context read it at wsg_create (wsg_mgpu.cpp)
+bool ctx_multi_share(const wsg_ctx* c);
 
 } // namespace wsg

@@ -229,8 +229,7 @@ void on_contexts(wsg_ctx* const* ctxs, int parts, Fn fn)
 // context (the one-GPU tests exercise the split that way).
 std::vector<wsg_ctx*> one_per_device(wsg_ctx* const* ctxs, int nctx)
 {
-    const char* e = wsg::envp("WSG_HOST_MULTI_SHARE");
-    const bool share = e && *e == '1';
+    const bool share = nctx > 0 && wsg::ctx_multi_share(ctxs[0]);   // (read at wsg_create, not per call)
     std::vector<wsg_ctx*> v;
     std::vector<int> seen;
     for (int i = 0; i < nctx; ++i) {
