@@ -11,6 +11,11 @@ request may wait ($WSG_LANE_TIMEOUT_MS):
   the buffers being touched — not by the launch path, and not by the late
   lane once it runs — and the context refuses further calls.
 
+* handover: the lane made to hand over constantly ($WSG_LANE_YIELD_US and
+  $WSG_LANE_IDLE_US of tens of microseconds) while eight threads, each with
+  its own context, decode, encode and XOR through it: every result exact,
+  hundreds of launches, no request lost across a hand-over.
+
 Prints one JSON line {"ok": bool, ...}."""
 import json
 import os
@@ -37,8 +42,68 @@ def batch(seed):
     return wire, off[:-1].copy()
 
 
+def handover(res):
+    import threading
+
+    import oracle as orc
+
+    n_threads, rounds = 8, 40
+    codecs = [ca.Codec(0) for _ in range(n_threads)]
+    errors = []
+
+    def work(i):
+        try:
+            c = codecs[i]
+            rng = np.random.default_rng(700 + i)
+            pin_p, pin_w = ca.pinned_empty(1 << 17), ca.pinned_empty(1 << 17)
+            pin_in, pin_out = ca.pinned_empty(1 << 17), ca.pinned_empty(1 << 17)
+            for it in range(rounds):
+                desc, total = wl.ragged_desc(rng, rng.integers(0, 300, int(rng.integers(1, 1500))))
+                desc["mask"] = rng.random(len(desc)) < 0.9
+                payload = wl.random_bytes(rng, total + 16)
+                wire_o, off_o = orc.encode_batch(payload, desc)
+                if len(wire_o) > 60000:
+                    continue
+                pin_p[: len(payload)] = payload
+                rc, wire, off = c.encode_batch_host(pin_p[: len(payload)], desc, wire=pin_w)
+                if rc != 0 or not np.array_equal(wire, wire_o):
+                    errors.append(("encode", i, it, rc))
+                    return
+                fs = off_o[:-1].copy()
+                rc_o, out_o, _ = orc.decode_batch(wire_o, fs)
+                pin_in[: len(wire_o)] = wire_o
+                rc, out, _ = c.decode_batch_host(pin_in[: len(wire_o)], fs, out=pin_out)
+                if rc != rc_o or not np.array_equal(out[: len(wire_o)], out_o):
+                    errors.append(("decode", i, it, rc))
+                    return
+                data = bytes(wl.random_bytes(rng, int(rng.integers(1, 100))))
+                key = int(rng.integers(0, 2**32))
+                kb = np.frombuffer(key.to_bytes(4, "little"), np.uint8)
+                ref = np.frombuffer(data, np.uint8) ^ kb[np.arange(len(data)) % 4]
+                if not np.array_equal(np.frombuffer(c.xor_host(data, key, 0), np.uint8), ref):
+                    errors.append(("xor", i, it))
+                    return
+        except Exception as e:
+            errors.append(("exception", i, repr(e)))
+
+    threads = [threading.Thread(target=work, args=(i,)) for i in range(n_threads)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    stats = [c.lane_stats() for c in codecs]
+    res.update(errors=errors[:5], alive=sum(th.is_alive() for th in threads), launches=stats[0][1],
+               requests=sum(s[0] for s in stats), running=stats[0][2])
+    res["ok"] = bool(not errors and res["alive"] == 0 and res["launches"] >= 50 and res["running"] != -1)
+    for c in codecs:
+        c.close()
+    print(json.dumps(res))
+
+
 def main():
     case = sys.argv[1]
+    if case == "handover":
+        return handover({"case": case})
     res = {"case": case}
     c = ca.Codec(0)
     wire, fs = batch(1)
