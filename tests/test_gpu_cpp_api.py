@@ -44,3 +44,47 @@ def test_echo_c1_modes(mode, clients, threads):
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["payload_ok"] is True
     assert d["total_messages"] >= clients * 100
+
+
+def test_per_call_path_on_the_lane_vs_oracle():
+    """The per-call path (PrepareSendFrame / PrepareReceiveFrame outside a
+    batch scope: what `Send*Async` from a non-IO thread and every sync `Send*`
+    run, reference examples/ws_chat_client.cpp:131) through the C-ABI's
+    per-connection codec: every masked payload is one task on the device's
+    lane (the context's lane request count grows by one per masked payload),
+    and every frame and every receive callback equals the oracle's.  Payloads
+    of 0-80 bytes (inline in the task up to 40) and up to 70 KB (staged; over
+    64 KiB the launch path)."""
+    import numpy as np
+
+    import cppserver_amd as ca
+    import oracle
+
+    rng = np.random.default_rng(77)
+    codec = ca.Codec(0)
+    try:
+        prod, ref = ca.Session(codec), oracle.Session()
+        rx_p, rx_r = ca.Session(codec), oracle.Session()
+        r0, _, _ = codec.lane_stats()
+        masked = 0
+        for i in range(400):
+            n = int(rng.integers(0, 81)) if i % 4 else int(rng.choice([300, 4000, 65536, 70000]))
+            payload = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            key = int(rng.integers(1, 2**32))
+            op = int(rng.choice([0x81, 0x82, 0x89, 0x8A, 0x88]))
+            status = 1000 if op == 0x88 else 0
+            prod.set_send_key(key)
+            ref.set_send_key(key)
+            frame = prod.prepare_send(op, True, payload, status)
+            assert frame == ref.prepare_send(op, True, payload, status), i
+            rx_p.prepare_receive(frame)
+            rx_r.prepare_receive(frame)
+            assert rx_p.events() == rx_r.events(), i
+            _, h = ca.header_unpack(frame)
+            body = len(frame) - int(h["hdr_len"])
+            if 0 < body <= 65536:
+                masked += 2   # the send's mask and the receive's unmask
+        r1, _, _ = codec.lane_stats()
+        assert r1 - r0 == masked, (r1 - r0, masked)
+    finally:
+        codec.close()
