@@ -798,6 +798,14 @@ int wsg_destroy(wsg_ctx* c)
 {
     if (!c)
         return WSG_EINVAL;
+    if (c->dead) {
+        // a lane request of this context neither answered nor drained: the
+        // lane may still write its page-locked buffers, and freeing device or
+        // page-locked memory waits for a device that may never drain; its
+        // memory is left to the process's end
+        delete c;
+        return WSG_OK;
+    }
     (void)hipSetDevice(c->device);
     if (c->stream)
         (void)hipStreamSynchronize(c->stream);

@@ -133,6 +133,7 @@ def main():
         untouched = bool(np.all(np.array(pin_out) == 0xEE))
         rc2, _, _ = c.decode_batch_host(pin_in, fs, out=pin_out)
         res.update(untouched=untouched, rc_after=rc2)
+        c.close()   # (a dead context: its buffers are left to the process's end, not freed under the lane)
         res["ok"] = bool(rc == WSG_EHIP and untouched and rc2 == WSG_EHIP)
     print(json.dumps(res))
 
