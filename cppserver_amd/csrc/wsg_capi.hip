@@ -1018,9 +1018,7 @@ int fanout_one_flat(wsg_ctx* c, hipStream_t s, const uint8_t* d_payload, uint64_
 {
     const uint64_t fsize = wsg_frame_size(opcode, mask, len, 0);
     const uint64_t total = fsize * k;
-    const uint64_t pieces = uint64_t(k) * ((fsize + wsg::PIECE_ALIGN - 1 + wsg::PIECE - 1) / wsg::PIECE);
-    const uint64_t blocks = wsg::fanout_flat ? ceil_div(ceil_div(total, wsg::CHUNK), wsg::BLOCK * wsg::FAN_UNITS)
-                                             : ceil_div(pieces, wsg::BLOCK / 64);
+    const uint64_t blocks = ceil_div(ceil_div(total, wsg::CHUNK), wsg::BLOCK * wsg::FAN_UNITS);
     WSG_HIP(wsg::launch_fanout(s, grid_for(c, blocks), d_payload, len, d_keys, k, opcode, mask ? 1u : 0u, fsize,
                                d_wire));
     return WSG_OK;

@@ -22,10 +22,6 @@ constexpr uint64_t PIECE = uint64_t(64) * CHUNK * EU;   // encode work piece: 4 
 // store row of a wave writes whole lines (a 16-B-aligned but line-misaligned
 // streaming store costs 6-16 %: tools/membench.hip explore, delta 16/80).
 constexpr uint64_t PIECE_ALIGN = 128;
-#ifndef WSG_FANOUT_FLAT
-#define WSG_FANOUT_FLAT 1
-#endif
-constexpr bool fanout_flat = WSG_FANOUT_FLAT != 0;       // fan-out: flat chunk stream (else per-frame pieces)
 #ifndef WSG_FAN_UNITS
 #define WSG_FAN_UNITS 4
 #endif

@@ -44,9 +44,6 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_ENC_NT_HI
 #define WSG_ENC_NT_HI 1    // ... including the funnel's second block (the next lane's line)
 #endif
-#ifndef WSG_ENC_EDGE
-#define WSG_ENC_EDGE 2   // k_encode_mask non-data chunks: 2 vector build + dword stores (edge_chunk2), 1 the byte loop (edge_chunk, A/B): C3 0.730 -> 0.701 ms (profiles/r4/edge2_diag.log)
-#endif
 #ifndef WSG_DIAG_ENC
 #define WSG_DIAG_ENC 0   // timing-only encode diagnostics: 1 skip edge chunks, 2 no funnel
 #endif
@@ -65,20 +62,8 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_DEC_RELOAD
 #define WSG_DEC_RELOAD 1   // k_decode staged tiles re-read their bytes instead of holding them in registers
 #endif
-#ifndef WSG_DEC_INFO_LAST
-#define WSG_DEC_INFO_LAST 0   // k_decode: per-frame info slice after the tiles, on the grid's last blocks (A/B)
-#endif
-#ifndef WSG_DEC_PAIR
-#define WSG_DEC_PAIR 0   // k_decode: two tiles per block, both loaded up front (A/B with WSG_DEC_TILES_PER_BLOCK=2)
-#endif
 #ifndef WSG_FAN_PERIOD
 #define WSG_FAN_PERIOD 1   // fan-out: period path (k_fanout_period) where the frame size allows; 0 = flat kernel only
-#endif
-#ifndef WSG_FAN_PRO
-#define WSG_FAN_PRO 1   // fan-out period path prologue (A/B, tools/c4_ab.py): 1 all kernel arguments loaded in one round, 2 both payload windows issued together branch-free, 4 early exit past the last row
-#endif
-#ifndef WSG_FAN_KSEL
-#define WSG_FAN_KSEL 2   // fan-out period path: a pass's keys by ds_bpermute one pass ahead (2: C4 8.32 vs 8.40 us) or in the pass (0); v_readlane + per-lane selects measured 8.6 us (round 3)
 #endif
 #ifndef WSG_FAN_UNROLL
 #define WSG_FAN_UNROLL 1   // fan-out period path: passes per loop iteration (A/B)
@@ -764,14 +749,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
                                                   uint32_t stride, wsg_recv_info* __restrict__ info,
                                                   unsigned long long* err, uint64_t num_tiles)
 {
-    // per-frame slice: header unpack + checks, one lane per frame.
-    // WSG_DEC_INFO_LAST: run by the grid's last blocks after their tiles
-    // (the first blocks of a grid smaller than the tile count stream two
-    // tiles each, so frames there would lengthen the longest blocks)
-    auto info_slice = [&]() {
+    // per-frame slice: header unpack + checks, one lane per frame (on the
+    // grid's last blocks after their tiles instead: no faster, round 3)
+    {
         const uint64_t fstride = uint64_t(gridDim.x) * BLOCK;
-        const uint64_t vb = WSG_DEC_INFO_LAST ? uint64_t(gridDim.x - 1 - blockIdx.x) : uint64_t(blockIdx.x);
-        for (uint64_t i0 = vb * BLOCK + (threadIdx.x & ~63u); i0 < n && !WSG_DIAG_NOINFO; i0 += fstride) {
+        for (uint64_t i0 = uint64_t(blockIdx.x) * BLOCK + (threadIdx.x & ~63u); i0 < n && !WSG_DIAG_NOINFO;
+             i0 += fstride) {
             const uint64_t i = i0 + (threadIdx.x & 63u);
             if (i < n) {
                 wsg_recv_info r;
@@ -781,9 +764,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
                 store_info(info + i, r);
             }
         }
-    };
-    if (!WSG_DEC_INFO_LAST)
-        info_slice();
+    }
 
 #if WSG_DIAG == 6   // timing-only: the launch as a bare copy-with-XOR of the full tiles (no frame logic)
     for (uint64_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
@@ -804,27 +785,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WSG_DEC_W
     }
     return;
 #endif
-#if WSG_DEC_PAIR
-    // two tiles per block, both tiles' loads in flight before the first
-    // tile's metadata chain (separate registers: the second tile's loads do
-    // not wait for the first one's stores); host grid: ceil(tiles / 2)
-    for (uint64_t t = 2 * uint64_t(blockIdx.x); t < num_tiles; t += 2 * uint64_t(gridDim.x)) {
-        TileIn a, b;
-        load_tile(a, wire, wire_len, fs, n, frames_per_byte, stride, t * TILE);
-        load_tile(b, wire, wire_len, fs, n, frames_per_byte, stride, min(t + 1, num_tiles - 1) * TILE);
-        process_tile(a, wire, out, wire_len, fs, n, stride);
-        if (t + 1 < num_tiles)
-            process_tile(b, wire, out, wire_len, fs, n, stride);
-    }
-#else
+    // (two tiles per block with both tiles' loads up front: 0.0900 vs 0.0875
+    // ms at C2, round 2, dropped)
     for (uint64_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
         TileIn a;
         load_tile(a, wire, wire_len, fs, n, frames_per_byte, stride, t * TILE);
         process_tile(a, wire, out, wire_len, fs, n, stride);
     }
-#endif
-    if (WSG_DEC_INFO_LAST)
-        info_slice();
 }
 
 // ===========================================================================
@@ -956,60 +923,6 @@ __device__ __forceinline__ v4u low_bytes(uint64_t n)   // bytes [0, n) = 0xFF
     return v4u{uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32)};
 }
 
-// A chunk of frame R that is not all data (it holds header / close-status
-// bytes, or it is shared with a neighbouring frame).  Its data bytes come
-// from one 32-byte source window read with at most two aligned 16-B loads
-// (only blocks that hold a byte of this frame's data are touched); all 16
-// bytes are built in registers, then stored with one 16-B store, or, for a
-// chunk shared with a neighbour, with byte stores of this frame's bytes only.
-// No load sits between two stores, so nothing here is a latency chain.
-__device__ __forceinline__ void edge_chunk(const FrameRec& R, uint64_t p, uint8_t* __restrict__ wire)
-{
-    // source of wire byte q: R.src + (q - R.data_w); offsets from R.src
-    // (pointer arithmetic on the payload argument keeps the loads global_*:
-    // through uintptr_t they became flat loads, which count on lgkmcnt too)
-    const int64_t rel = int64_t(p - R.data_w);   // source offset of wire byte p
-    const uint32_t s = uint32_t((reinterpret_cast<uintptr_t>(R.src) + uint64_t(rel)) & 15u);
-    const int64_t r0 = rel - int64_t(s);           // aligned block holding it, relative to R.src
-    const int64_t data_len = int64_t(R.end - R.data_w);
-    v4u lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
-    if (r0 < data_len && r0 + 16 > 0)
-        lo = ld16(R.src + r0);
-    if (s != 0 && r0 + 16 < data_len && r0 + 32 > 0)
-        hi = ld16(R.src + r0 + 16);
-    const v4u d = s ? funnel(lo, hi, s) : lo;   // byte j: source byte of wire byte p + j
-    v4u w = {0, 0, 0, 0};
-    uint32_t own = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < CHUNK; ++j) {
-        const uint64_t q = p + j;
-        if (q < R.off || q >= R.end)
-            continue;
-        own |= 1u << j;
-        uint32_t b;
-        if (q >= R.data_w) {
-            b = lane_byte(d, j) ^ key_byte(R.key, q - R.pw);
-        } else {
-            const uint64_t r = q - R.off;
-            if (r < R.hdr) {
-                b = header_byte(R.opcode, R.mask, R.body, R.key, uint32_t(r));
-            } else {
-                const uint64_t k = r - R.hdr;   // close-status byte 0 or 1
-                b = uint32_t((k == 0 ? (R.status >> 8) : R.status) & 0xFF) ^ key_byte(R.key, k);
-            }
-        }
-        put_byte(w, j, b);
-    }
-    if (own == 0xFFFFu || (WSG_DIAG_ENC & 4)) {   // DIAG 4: full stores for shared chunks (timing only)
-        st16nt(wire + p, w);
-    } else {
-#pragma unroll
-        for (uint32_t j = 0; j < CHUNK; ++j)
-            if ((own >> j) & 1u)
-                wire[p + j] = uint8_t(lane_byte(w, j));
-    }
-}
-
 // Header + close-status bytes of frame R (<= 16, as PrepareSendFrame writes
 // them, the status masked like payload bytes 0-1: SURVEY Q2/Q3), zero past
 // them; wave-uniform.
@@ -1113,7 +1026,7 @@ struct Piece {
         const uint32_t lane = threadIdx.x & 63;
         const OutTile ot(wire + lo, uint32_t(PIECE), WSG_ENC_SC1 != 0);
         v4u head = {0, 0, 0, 0};
-        if (WSG_ENC_EDGE == 2 && lo < R.data_w)   // (wave-uniform) the piece holds header / status bytes
+        if (lo < R.data_w)   // (wave-uniform) the piece holds header / status bytes
             head = frame_head(R);
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
@@ -1122,10 +1035,9 @@ struct Piece {
                 ot.put(uint32_t(p - lo), (s ? funnel(a[u], b[u], s) : a[u]) ^ kw);
             } else if (p < hi && !(WSG_DIAG_ENC & 1)) {
                 // header / status bytes, or a chunk shared with a neighbour
-                if (WSG_ENC_EDGE == 2)
-                    edge_chunk2(R, head, p, wire);
-                else
-                    edge_chunk(R, p, wire);
+                // (built as a vector: the byte-at-a-time build it replaced
+                // made C3's encode 0.730 ms against 0.701, round 4)
+                edge_chunk2(R, head, p, wire);
             }
         }
     }
@@ -1294,26 +1206,7 @@ __global__ __launch_bounds__(BLOCK) void k_encode_mask(const uint8_t* __restrict
     }
 }
 
-// k client-style frames of one payload (one key each), back to back: pieces
-// map to frames arithmetically.  The payload is re-read by every frame, so
-// its loads keep the default cache policy (it stays in L2).
-__global__ __launch_bounds__(BLOCK) void k_fanout(const uint8_t* __restrict__ payload, uint64_t len,
-                                                  const uint32_t* __restrict__ keys, uint32_t k, uint8_t opcode,
-                                                  uint32_t mask, uint64_t fsize, uint8_t* __restrict__ wire)
-{
-    const uint32_t per_frame = uint32_t(pieces_of(fsize));
-    const uint64_t pieces = uint64_t(per_frame) * k;
-    const uint64_t waves = uint64_t(gridDim.x) * (BLOCK / 64);
-    for (uint64_t q = uint64_t(blockIdx.x) * (BLOCK / 64) + wave_id(); q < pieces; q += waves) {
-        Piece<false> pc;
-        const uint32_t i = uint32_t(q / per_frame);
-        pc.load(make_rec(uint64_t(i) * fsize, payload, len, keys[i], 0, opcode, mask != 0),
-                q - uint64_t(i) * per_frame, true);
-        pc.store(wire);
-    }
-}
-
-// Flat variant: the k frames are one byte stream of k * fsize bytes, cut into
+// Fan-out, flat kernel (frame sizes the period path does not take): the k frames are one byte stream of k * fsize bytes, cut into
 // 16-byte chunks; every lane builds whole chunks (both frames' bytes where a
 // frame boundary falls inside one), so every store is a full 16-B store and
 // no cache line is written in parts by two waves.  The frame of a chunk is
@@ -2064,51 +1957,6 @@ __device__ __forceinline__ void fan_tm(const uint8_t* __restrict__ payload, uint
         t |= fan_window(payload, len, int64_t(o) - int64_t(f.data0)) & (low_bytes(hi) & ~low_bytes(lo));
 }
 
-// fan_tm for two chunk offsets at once (a chunk's and a frame start's):
-// both payload windows' loads are issued before either is used, so they
-// come back in one memory round trip (fan_tm's own branches made the
-// compiler wait for the first pair before issuing the second)
-struct FanWin {
-    v4u lo, hi;
-    uint32_t s;
-};
-__device__ __forceinline__ FanWin fan_window_issue(const uint8_t* __restrict__ payload, uint64_t len, int64_t c)
-{
-    // branch-free: each load is issued unconditionally from a block clamped
-    // into the payload's own aligned blocks, and zeroed where fan_window
-    // would not have loaded it (a load under a branch made the compiler
-    // copy its result inside the branch, i.e. wait for it there); the
-    // period path has len >= 1 (host: G >= 64 needs frames of >= 512 B)
-    FanWin w;
-    const uintptr_t base = reinterpret_cast<uintptr_t>(payload);
-    w.s = uint32_t((base + uint64_t(c)) & 15u);
-    const int64_t r0 = c - int64_t(w.s);   // aligned block holding byte c, relative to payload
-    const int64_t n = int64_t(len);
-    const int64_t first = -int64_t(base & 15u);                                        // block of byte 0
-    const int64_t last = int64_t(((base + len - 1) & ~uintptr_t(15)) - base);         // block of byte len - 1
-    const int64_t r1 = r0 + 16;
-    const bool ok_lo = r0 < n && r0 + 16 > 0;
-    const bool ok_hi = r1 < n && r1 + 16 > 0;   // (unused at s = 0: funnel(lo, hi, 0) = lo)
-    const v4u a = ld16(payload + (r0 < first ? first : r0 > last ? last : r0));
-    const v4u b = ld16(payload + (r1 < first ? first : r1 > last ? last : r1));
-    const v4u z = {0, 0, 0, 0};
-    w.lo = ok_lo ? a : z;
-    w.hi = ok_hi ? b : z;
-    return w;
-}
-__device__ __forceinline__ void fan_tm_finish(const FanWin& w, const FanGeom& f, uint64_t fsize, uint64_t o, v4u& t,
-                                              v4u& m)
-{
-    const uint64_t hi = fsize - o < CHUNK ? fsize - o : CHUNK;
-    const uint64_t kl = o < f.kpos ? f.kpos - o : 0;
-    const uint64_t lo = o < f.data0 ? f.data0 - o : 0;
-    m = low_bytes(hi) & ~low_bytes(kl);
-    t = shr_bytes(f.hp0, o);
-    // no `if (lo < hi)`: the byte mask is empty then, and a branch here let
-    // the compiler sink the loads into it, behind a wait
-    t |= funnel(w.lo, w.hi, w.s) & (low_bytes(hi) & ~low_bytes(lo));
-}
-
 template <int P>
 __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restrict__ payload0, uint64_t len,
                                                       const uint32_t* __restrict__ keys, uint32_t k, uint8_t opcode,
@@ -2124,8 +1972,7 @@ __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restric
     // compiler, the argument loads came in five dependent rounds (each
     // waiting on the last), a visible share of a 9 us kernel; this empty
     // asm consumes them all, so they are issued together and waited once
-    if (WSG_FAN_PRO & 1)
-        asm volatile("" ::"s"(payload0), "s"(len), "s"(keys), "s"(k), "s"(fsize), "s"(G), "s"(dm), "s"(wire0),
+    asm volatile("" ::"s"(payload0), "s"(len), "s"(keys), "s"(k), "s"(fsize), "s"(G), "s"(dm), "s"(wire0),
                      "s"(nwaves), "s"(wpb), "s"(src_off), "s"(dst_off), "s"(uint32_t(opcode)), "s"(mask));
     const uint8_t* __restrict__ payload = payload0 + src_off;
     uint8_t* __restrict__ wire = wire0 + dst_off;
@@ -2147,8 +1994,6 @@ __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restric
         return;
     const uint64_t row0 = uint64_t(wid) * 64;
     const uint64_t rstep = uint64_t(nwaves) * 64;   // W rows: a multiple of G (dm groups)
-    if ((WSG_FAN_PRO & 4) && row0 >= chunks)   // a wave past the last row (its loads are guarded anyway)
-        return;
     const uint64_t m0 = uint32_t(row0) / G;              // first group of pass 0 (host: W < 2^22, row0 < 2^28)
     const uint32_t jw = uint32_t(row0 - m0 * G);         // group position of lane 0
     const uint32_t dl = (jw + lane) >= G ? 1u : 0u;      // lane's group: m0 + dl (+ it * dm)
@@ -2181,22 +2026,14 @@ __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restric
     // lane so that its payload loads go out with the chunk's own instead of
     // in a second round behind them; used where a frame starts in the chunk
     const uint64_t split = fsize - r;                    // the next frame starts at chunk byte `split`
-    if (WSG_FAN_PRO & 2) {
+    // (both windows issued together branch-free instead: +0.5 us per C4,
+    // every lane then loads two more blocks; round 3)
+    fan_tm(payload, len, f, fsize, r, t, ma);
+    if (split < CHUNK) {
         v4u t0, m0v;
-        const FanWin wa = fan_window_issue(payload, len, int64_t(r) - int64_t(f.data0));
-        const FanWin wb = fan_window_issue(payload, len, -int64_t(f.data0));
-        fan_tm_finish(wb, f, fsize, 0, t0, m0v);
-        fan_tm_finish(wa, f, fsize, r, t, ma);
-        t |= shl_bytes(t0, split);                       // (zero unless split < CHUNK; no branch, see above)
+        fan_tm(payload, len, f, fsize, 0, t0, m0v);
+        t |= shl_bytes(t0, split);
         mb = shl_bytes(m0v, split);
-    } else {
-        fan_tm(payload, len, f, fsize, r, t, ma);
-        if (split < CHUNK) {
-            v4u t0, m0v;
-            fan_tm(payload, len, f, fsize, 0, t0, m0v);
-            t |= shl_bytes(t0, split);
-            mb = shl_bytes(m0v, split);
-        }
     }
     if (WSG_DIAG_FAN & 16) {
         t = v4u{j, 1, 2, 3};
@@ -2242,20 +2079,15 @@ __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restric
     // masking; the loop is VALU-bound once the shuffles are off its chain.
     auto passes = [&](auto has_b) {
         constexpr bool B = decltype(has_b)::value;
+        // a pass's keys are shuffled one pass ahead (in the pass itself:
+        // C4 8.40 vs 8.32 us; v_readlane + per-lane selects 8.6, round 3)
         uint32_t ka_n = 0, kb_n = 0;
-        if (WSG_FAN_KSEL == 2)
-            pass_keys(0, ka_n, kb_n, B);
+        pass_keys(0, ka_n, kb_n, B);
         auto word = [&](uint32_t it) {
-            uint32_t ka, kb;
-            if (WSG_FAN_KSEL == 2) {
-                // this pass's keys were shuffled during the previous pass;
-                // the next pass's go out now, ahead of this pass's store
-                ka = ka_n;
-                kb = kb_n;
-                pass_keys(it + 1, ka_n, kb_n, B);   // (past the last pass: slots of kv, unused)
-            } else {
-                pass_keys(it, ka, kb, B);
-            }
+            // this pass's keys were shuffled during the previous pass; the
+            // next pass's go out now, ahead of this pass's store
+            const uint32_t ka = ka_n, kb = kb_n;
+            pass_keys(it + 1, ka_n, kb_n, B);   // (past the last pass: slots of kv, unused)
             const uint32_t ra = __builtin_amdgcn_alignbit(ka, ka, sa);
             v4u w = t ^ (ma & v4u{ra, ra, ra, ra});
             if constexpr (B) {
@@ -2380,16 +2212,11 @@ hipError_t launch_encode_small(hipStream_t s, const uint8_t* payload, const wsg_
 hipError_t launch_fanout(hipStream_t s, int grid, const uint8_t* payload, uint64_t len, const uint32_t* keys,
                          uint32_t k, uint8_t opcode, uint32_t mask, uint64_t fsize, uint8_t* wire)
 {
-    if (fanout_flat)
-    {
-        // edge blocks: two items per frame start (k + 1 starts); none for
-        // frames shorter than a chunk (the streaming waves do those)
-        const uint64_t edge_blocks = fsize >= CHUNK ? (2 * (uint64_t(k) + 1) + BLOCK - 1) / BLOCK : 0;
-        k_fanout_flat<<<dim3(uint32_t(grid + edge_blocks)), BLOCK, 0, s>>>(
-            payload, len, keys, k, opcode, mask, fsize, 1.0 / double(fsize), uint32_t(grid), wire);
-    }
-    else
-        k_fanout<<<grid, BLOCK, 0, s>>>(payload, len, keys, k, opcode, mask, fsize, wire);
+    // edge blocks: two items per frame start (k + 1 starts); none for
+    // frames shorter than a chunk (the streaming waves do those)
+    const uint64_t edge_blocks = fsize >= CHUNK ? (2 * (uint64_t(k) + 1) + BLOCK - 1) / BLOCK : 0;
+    k_fanout_flat<<<dim3(uint32_t(grid + edge_blocks)), BLOCK, 0, s>>>(
+        payload, len, keys, k, opcode, mask, fsize, 1.0 / double(fsize), uint32_t(grid), wire);
     return hipGetLastError();
 }
 
