@@ -11,7 +11,9 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <new>
@@ -1190,7 +1192,103 @@ int wsg_xor_host(wsg_ctx* c, const void* src, void* dst, size_t len, uint32_t ke
     return WSG_OK;
 }
 
+#ifndef WSG_COPY_WORKERS
+#define WSG_COPY_WORKERS 5   // worker threads of the staged pipelines' host copies (A/B: tools/pcie_pageable.py)
+#endif
+
 namespace {
+
+// Large host copies of the staged pipelines (a pageable caller buffer to or
+// from the page-locked staging): one core copies ~27 GB/s, and a decode from
+// pageable memory makes two such copies per byte (in and out), so one thread
+// held the pipeline to 12.9 GiB/s of payload against 40 for page-locked
+// buffers (round 4's bench line).  Copies of at least two parts' worth are
+// cut into parts done by the calling thread and a few workers (made on first
+// use; they park on the queue and are left to the process's end).
+class CopyPool
+{
+public:
+    static CopyPool& get()
+    {
+        static CopyPool* p = new CopyPool;   // leaked: its workers stay parked until the process ends
+        return *p;
+    }
+    void copy(void* dst, const void* src, size_t len)
+    {
+        const size_t parts = std::min<size_t>(kWorkers + 1, len / kPartMin);
+        if (parts <= 1) {
+            std::memcpy(dst, src, len);
+            return;
+        }
+        start_workers();
+        const size_t per = ((len + parts - 1) / parts + 63) & ~size_t(63);
+        std::atomic<size_t> left{0};
+        size_t n = 0;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            for (size_t at = per; at < len; at += per, ++n)
+                q_.push_back(Job{static_cast<uint8_t*>(dst) + at, static_cast<const uint8_t*>(src) + at,
+                                 std::min(per, len - at), &left});
+            left.store(n, std::memory_order_relaxed);
+        }
+        cv_.notify_all();
+        std::memcpy(dst, src, std::min(per, len));
+        // then help with whatever is queued (this call's parts or another's)
+        // and wait for this call's parts
+        for (;;) {
+            Job j{};
+            {
+                std::lock_guard<std::mutex> g(m_);
+                if (q_.empty())
+                    break;
+                j = q_.back();
+                q_.pop_back();
+            }
+            run(j);
+        }
+        while (left.load(std::memory_order_acquire) != 0)
+            std::this_thread::yield();
+    }
+
+private:
+    static constexpr size_t kWorkers = WSG_COPY_WORKERS;
+    static constexpr size_t kPartMin = size_t(2) << 20;
+    struct Job {
+        uint8_t* dst;
+        const uint8_t* src;
+        size_t len;
+        std::atomic<size_t>* left;
+    };
+    static void run(const Job& j)
+    {
+        std::memcpy(j.dst, j.src, j.len);
+        j.left->fetch_sub(1, std::memory_order_acq_rel);
+    }
+    void start_workers()
+    {
+        std::call_once(once_, [this] {
+            for (size_t i = 0; i < kWorkers; ++i)
+                std::thread([this] {
+                    for (;;) {
+                        Job j;
+                        {
+                            std::unique_lock<std::mutex> g(m_);
+                            cv_.wait(g, [this] { return !q_.empty(); });
+                            j = q_.front();
+                            q_.pop_front();
+                        }
+                        run(j);
+                    }
+                }).detach();
+        });
+    }
+    std::once_flag once_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<Job> q_;
+};
+
+void host_copy(void* dst, const void* src, size_t len) { CopyPool::get().copy(dst, src, len); }
 
 bool host_pinned(const void* p)
 {
@@ -1316,7 +1414,7 @@ int slot_drain(wsg_ctx::Slot& sl)
         return WSG_OK;
     WSG_HIP(hipEventSynchronize(sl.done));
     if (sl.out_dst && sl.out_len)
-        std::memcpy(sl.out_dst, sl.h_out + sl.out_src, sl.out_len);
+        host_copy(sl.out_dst, sl.h_out + sl.out_src, sl.out_len);
     for (uint32_t k = 0; k < sl.info_n; ++k) {
         wsg_recv_info r = sl.h_info[k];
         r.payload_off += sl.base;   // segment-relative -> wire offset
@@ -1515,7 +1613,7 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
                 sl.h_fs[j] = frame_start[i0 + j] >= base ? frame_start[i0 + j] - base : ~uint64_t(0);
             const uint8_t* src = wire + base;
             if (!in_pinned) {
-                std::memcpy(sl.h_in, wire + base, len);
+                host_copy(sl.h_in, wire + base, len);
                 src = sl.h_in;
             }
             Pipe pp;
@@ -1763,7 +1861,7 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
                     sl.h_desc[j] = d;
                 }
                 if (!in_pinned && plen) {
-                    std::memcpy(sl.h_in, src, plen);
+                    host_copy(sl.h_in, src, plen);
                     src = sl.h_in;
                 }
             }
