@@ -393,7 +393,8 @@ def test_lane_per_call_xor(lane, launch):
     phase, against a numpy restatement of ws.cpp:264-270."""
     rng = np.random.default_rng(41)
     r0, _, _ = lane.lane_stats()
-    lens = [1, 2, 3, 15, 16, 17, 31, 32, 33, 125, 126, 1000, 4095, 4096, 4097, 16383, 65535, 65536, 65537, 200000]
+    lens = [1, 2, 3, 15, 16, 17, 31, 32, 33, 39, 40, 41, 63, 64, 125, 126, 1000, 4095, 4096, 4097, 16383, 16384,
+            16385, 65535, 65536, 65537, 200000]   # (up to 40: the payload inside the task)
     for ln in lens:
         for phase in range(4):
             data = wl.random_bytes(rng, ln)
