@@ -686,10 +686,9 @@ def echo_c1_leg(seconds=3.0, timeout=120):
     tcp = os.path.join(ROOT, "tools", "_build", "bench_echo_tcp")
     if os.path.exists(tcp):
         tr = {}
-        # gpu_100c_4t_hwq8: the same with one hardware queue per IO thread
-        # (GPU_MAX_HW_QUEUES=8 for the 4 server + 4 client threads; the
-        # library then gives each thread's context a lane): a runtime setting
-        # of the deployment, reported beside the default one
+        # gpu_100c_4t_hwq8: the same with GPU_MAX_HW_QUEUES=8 (round 4's
+        # per-context lanes needed a hardware queue per IO thread; the one
+        # lane per device of round 5 does not: the two should match)
         for leg, a, env in (("gpu_1c_1t", ["gpu", "1", "1"], None), ("gpu_100c_4t", ["gpu", "100", "4"], None),
                             ("gpu_100c_4t_hwq8", ["gpu", "100", "4"], {"GPU_MAX_HW_QUEUES": "8"}),
                             ("gpu_tick_100c_4t", ["gpu_tick", "100", "4"], None),
