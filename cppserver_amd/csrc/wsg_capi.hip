@@ -569,8 +569,10 @@ enum LaneResult { LANE_DONE = 0, LANE_FALLBACK = 1, LANE_LOST = 2 };
 // was given up — their outputs are written).  LANE_LOST: given up and the lane
 // did not leave in time: it may still write the request's buffers, so the
 // caller must not reuse them (the context is marked dead).
+// xwords > 0: one inline-XOR task, answered by its self-tagged units
+// (wsg::LaneXres), whose dwords go to xout.
 LaneResult lane_run(wsg_ctx* c, LaneServer* s, const uint64_t (*words)[wsg::LANE_WORDS], uint32_t groups,
-                    uint64_t* errs, uint32_t* answered)
+                    uint64_t* errs, uint32_t* answered, uint32_t xwords = 0, uint32_t* xout = nullptr)
 {
     *errs = 0;
     *answered = 0;
@@ -611,10 +613,23 @@ LaneResult lane_run(wsg_ctx* c, LaneServer* s, const uint64_t (*words)[wsg::LANE
         while (k < groups) {
             const uint64_t tk = x + k;
             const uint32_t wg = uint32_t(tk % W), slot = uint32_t((tk / W) % R);
-            wsg::LaneResp& r = s->bell->resp[wg][slot];
-            if (__atomic_load_n(&r.done, __ATOMIC_ACQUIRE) != tk + 1)
-                break;
-            *errs += __atomic_load_n(&r.errs, __ATOMIC_RELAXED);
+            if (xwords) {   // (one group) every unit shows the tag: the answer is complete
+                const wsg::LaneXres& xr = s->bell->xres[wg][slot];
+                uint32_t q = 0;
+                for (; q < xwords; ++q) {
+                    const uint64_t u = __atomic_load_n(&xr.u[q], __ATOMIC_ACQUIRE);
+                    if (uint32_t(u >> 32) != uint32_t(tk + 1))
+                        break;
+                    xout[q] = uint32_t(u);
+                }
+                if (q < xwords)
+                    break;
+            } else {
+                wsg::LaneResp& r = s->bell->resp[wg][slot];
+                if (__atomic_load_n(&r.done, __ATOMIC_ACQUIRE) != tk + 1)
+                    break;
+                *errs += __atomic_load_n(&r.errs, __ATOMIC_RELAXED);
+            }
             s->released[wg * R + slot].store(tk + 1, std::memory_order_release);
             ++k;
         }
@@ -644,7 +659,8 @@ LaneResult lane_run(wsg_ctx* c, LaneServer* s, const uint64_t (*words)[wsg::LANE
     for (uint32_t q = 0; q < groups; ++q) {
         const uint64_t tk = x + q;
         const uint32_t wg = uint32_t(tk % W), slot = uint32_t((tk / W) % R);
-        if (__atomic_load_n(&s->bell->resp[wg][slot].done, __ATOMIC_ACQUIRE) == tk + 1)
+        if (xwords ? uint32_t(__atomic_load_n(&s->bell->xres[wg][slot].u[0], __ATOMIC_ACQUIRE) >> 32) == uint32_t(tk + 1)
+                   : __atomic_load_n(&s->bell->resp[wg][slot].done, __ATOMIC_ACQUIRE) == tk + 1)
             ++*answered;
         s->released[wg * R + slot].store(tk + 1, std::memory_order_release);
     }
@@ -1157,7 +1173,8 @@ int wsg_xor_host(wsg_ctx* c, const void* src, void* dst, size_t len, uint32_t ke
             uint64_t w[1][wsg::LANE_WORDS] = {{wsg::LANE_XOR | (uint64_t(1) << 32),
                                                reinterpret_cast<uint64_t>(c->h_stage), uint64_t(len),
                                                uint64_t(key) | (uint64_t(phase & 3u) << 32), 0, 0, 0, 0, 0}};
-            if (len <= wsg::LANE_INLINE) {
+            const bool inl = len <= wsg::LANE_INLINE;
+            if (inl) {   // (the answer comes back in the slot's self-tagged units, no buffer)
                 w[0][0] = wsg::LANE_XOR_INLINE | (uint64_t(1) << 32);
                 std::memcpy(&w[0][4], src, len);
             } else {
@@ -1165,9 +1182,11 @@ int wsg_xor_host(wsg_ctx* c, const void* src, void* dst, size_t len, uint32_t ke
             }
             uint64_t errs = 0;
             uint32_t answered = 0;
-            const LaneResult r = lane_run(c, ls, w, 1, &errs, &answered);
+            uint32_t res[wsg::LANE_INLINE / 4];
+            const LaneResult r = inl ? lane_run(c, ls, w, 1, &errs, &answered, uint32_t((len + 3) / 4), res)
+                                     : lane_run(c, ls, w, 1, &errs, &answered);
             if (r == LANE_DONE) {
-                std::memcpy(dst, c->h_stage, len);
+                std::memcpy(dst, inl ? static_cast<const void*>(res) : c->h_stage, len);
                 return WSG_OK;
             }
             if (r == LANE_LOST)

@@ -144,7 +144,8 @@ struct alignas(16) LaneUnit {
 //   xor:    w[1..3] = buffer, length, key | phase << 32 (n = 1): the
 //           page-locked buffer XORed in place, byte i with key byte
 //           (phase + i) % 4; LANE_XOR_INLINE: the payload (<= LANE_INLINE
-//           bytes) in w[4..8], the result written to the buffer
+//           bytes) in w[4..8], the result in the slot's LaneXres (no write
+//           to the buffer, no fence, no `done`)
 struct LaneTask {
     LaneUnit w[LANE_WORDS];
     uint64_t pad[2];
@@ -153,6 +154,14 @@ struct LaneTask {
 // done = the task's tag (release).
 struct alignas(16) LaneResp {
     uint64_t done, errs;
+};
+// The answer of an inline XOR: result dword k beside the low 32 bits of the
+// task's tag, one 8-byte unit each, written by one lane with one store and
+// read by the host with one load — a unit showing the tag holds its dword,
+// so the answer needs no release fence before it (the fence waits for the
+// stores to be acknowledged over PCIe).
+struct alignas(16) LaneXres {
+    uint64_t u[LANE_INLINE / 4];
 };
 struct alignas(16) LaneCtl {
     uint32_t stop;      // host: every workgroup leaves at its next check
@@ -163,6 +172,7 @@ struct LaneBell {
     LaneCtl ctl;
     uint64_t next_j[LANE_WGS_MAX];             // lane: workgroup g's next mailbox position (stored as it leaves)
     LaneResp resp[LANE_WGS_MAX][LANE_RING];    // lane: answers
+    LaneXres xres[LANE_WGS_MAX][LANE_RING];    // lane: inline XOR answers
     LaneTask box[LANE_WGS_MAX][LANE_RING];     // host: mailboxes (ticket x: box[x % W][(x / W) % LANE_RING])
 };
 // A launch of `workgroups` (the server's W) workgroups of generation `gen`

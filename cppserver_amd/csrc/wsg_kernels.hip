@@ -1757,12 +1757,21 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
                         reinterpret_cast<const uint64_t*>(s_w[3]), reinterpret_cast<uint8_t*>(s_w[4]), lds);
         else if (op == LANE_XOR && s_w[2] <= LANE_PSTAGE)
             lane_xor(reinterpret_cast<uint8_t*>(s_w[1]), s_w[2], uint32_t(s_w[3]), uint32_t(s_w[3] >> 32));
-        else if (op == LANE_XOR_INLINE && s_w[2] <= LANE_INLINE && t < (s_w[2] + 3) / 4) {
-            // the payload came with the task (w[4..8]): one dword per lane,
-            // written to the buffer (rounded up to whole dwords: the stage
-            // has the room), no read of host memory
-            const uint32_t d = uint32_t(s_w[4 + t / 2] >> (32 * (t & 1)));
-            reinterpret_cast<uint32_t*>(s_w[1])[t] = d ^ key_rot(uint32_t(s_w[3]), uint32_t(s_w[3] >> 32));
+        else if (op == LANE_XOR_INLINE) {
+            // the payload came with the task (w[4..8]) and the answer goes
+            // back as self-tagged units (LaneXres): one dword per lane, one
+            // 8-byte store each, no read of host memory and no fence
+            if (s_w[2] <= LANE_INLINE && t < (s_w[2] + 3) / 4) {
+                const uint32_t d = uint32_t(s_w[4 + t / 2] >> (32 * (t & 1)));
+                const uint32_t tag = uint32_t(uint64_t(g) + j * W + 1);
+                const uint64_t unit = uint64_t(d ^ key_rot(uint32_t(s_w[3]), uint32_t(s_w[3] >> 32))) |
+                                      (uint64_t(tag) << 32);
+                __hip_atomic_store(&bell->xres[g][j % LANE_RING].u[t], unit, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            ++j;
+            __syncthreads();   // (every wave has read this task's words before wave 0 polls the next)
+            continue;          // (every thread: op is block-uniform)
         }
         __syncthreads();
         if (t == 0) {
