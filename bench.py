@@ -694,15 +694,30 @@ def echo_c1_leg(seconds=3.0, timeout=120):
                             ("gpu_tick_100c_4t", ["gpu_tick", "100", "4"], None),
                             ("cpu_ref_1c_1t", ["cpu_ref", "1", "1"], None),
                             ("cpu_ref_100c_4t", ["cpu_ref", "100", "4"], None)):
-            r = _run_leg([tcp] + a + ["1000", "32", str(seconds)], timeout, env)
-            if r.returncode != 0:
-                tr[leg] = {"error": (r.stderr or r.stdout).strip()[-300:]}
+            # the 100-client legs share the host's loopback stack with whatever
+            # else runs on the machine: three runs each, the median reported
+            # (the gpu and cpu_ref legs alike), every run's rate listed
+            runs = []
+            for _ in range(3 if a[1] == "100" and env is None else 1):
+                r = _run_leg([tcp] + a + ["1000", "32", str(seconds)], timeout, env)
+                if r.returncode != 0:
+                    runs = [{"error": (r.stderr or r.stdout).strip()[-300:]}]
+                    break
+                runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+            if "error" in runs[0]:
+                tr[leg] = runs[0]
                 continue
-            d = json.loads(r.stdout.strip().splitlines()[-1])
+            d = sorted(runs, key=lambda x: x["msg_per_s"])[len(runs) // 2]
             tr[leg] = {k: d[k] for k in ("msg_per_s", "MiB_per_s", "latency_ns", "total_messages", "payload_ok")}
+            tr[leg]["payload_ok"] = all(x["payload_ok"] for x in runs)
+            if len(runs) > 1:
+                tr[leg]["runs_msg_per_s"] = [x["msg_per_s"] for x in runs]
+            if a[0] != "cpu_ref":   # socket reads, lane requests and launches of the reported run
+                tr[leg]["lane"] = {k: d.get(k) for k in ("reads", "lane_requests", "lane_launches", "lane_state")}
         tr["what"] = ("ws_echo over TCP 127.0.0.1 (one process, server and client on their own epoll threads): "
                       "gpu = the drop-in WSClient/WSSession, cpu_ref = the oracle's restatement of the reference "
-                      "codec (no GPU); the published figures below are this method on an i7-4790K")
+                      "codec (no GPU); 100-client legs: median of 3 runs (runs_msg_per_s); the published figures below are "
+                      "this method on an i7-4790K")
         out["tcp_loopback"] = tr
     out["reference_published"] = {"msg_per_s_1c_1t": 160448, "msg_per_s_100c_4t": 594328,
                                   "wss_msg_per_s_1c_1t": 203343, "wss_msg_per_s_100c_4t": 818230,

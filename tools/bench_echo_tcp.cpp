@@ -216,8 +216,13 @@ void ref_cb(void* user, int kind, const uint8_t* data, size_t len, int)
 double seconds(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 
 // One IO thread: its connections' ends (client ends or server ends), one epoll set.
+// Per-run path counters: socket reads, and this process's lane use as the
+// IO threads' codec contexts saw it (wsg_lane_stats at each thread's end).
+std::atomic<uint64_t> g_reads{0}, g_lane_requests{0}, g_lane_launches{0};
+std::atomic<int> g_lane_state{2};   // lowest seen: -1 given up, 0 not running, 1 running (2: none read)
+
 void io_loop(std::vector<End*>& ends, bool tick, double secs, bool client_side, std::atomic<int>& done_clients,
-             int n_client_threads, double& elapsed)
+             int n_client_threads, double& elapsed, bool gpu)
 {
     const int ep = epoll_create1(0);
     if (ep < 0)
@@ -231,6 +236,7 @@ void io_loop(std::vector<End*>& ends, bool tick, double secs, bool client_side, 
     }
     std::vector<epoll_event> evs(256);
     std::vector<uint8_t> buf(1 << 16);
+    uint64_t reads = 0;
     const auto t0 = Clock::now();
     auto idle_since = Clock::now();
     for (;;) {
@@ -247,6 +253,7 @@ void io_loop(std::vector<End*>& ends, bool tick, double secs, bool client_side, 
                 for (;;) {   // drain the socket: every read is one onReceived (TCPSession::TryReceive)
                     const ssize_t r = ::recv(e->t.fd, buf.data(), buf.size(), 0);
                     if (r > 0) {
+                        ++reads;
                         e->on_bytes(buf.data(), size_t(r));
                         if (size_t(r) < buf.size())
                             break;
@@ -274,6 +281,20 @@ void io_loop(std::vector<End*>& ends, bool tick, double secs, bool client_side, 
             break;
     }
     ::close(ep);
+    g_reads.fetch_add(reads);
+    if (gpu) {
+        uint64_t rq = 0, la = 0;
+        int st = 0;
+        if (wsg_lane_stats(ThreadCodec(), &rq, &la, &st) == WSG_OK) {
+            g_lane_requests.fetch_add(rq);
+            uint64_t m = g_lane_launches.load();
+            while (la > m && !g_lane_launches.compare_exchange_weak(m, la)) {
+            }
+            int cur = g_lane_state.load();
+            while (st < cur && !g_lane_state.compare_exchange_weak(cur, st)) {
+            }
+        }
+    }
 }
 
 } // namespace
@@ -354,7 +375,7 @@ int main(int argc, char** argv)
             pool.emplace_back([&, t] {
                 try {
                     BatchScope::SetEnabled(true);
-                    io_loop(spart[size_t(t)], tick, secs, false, done, threads, unused[size_t(t)]);
+                    io_loop(spart[size_t(t)], tick, secs, false, done, threads, unused[size_t(t)], !ref);
                 } catch (const std::exception& e) {
                     errors[size_t(t)] = e.what();
                 }
@@ -362,7 +383,7 @@ int main(int argc, char** argv)
             pool.emplace_back([&, t] {
                 try {
                     BatchScope::SetEnabled(true);
-                    io_loop(cpart[size_t(t)], tick, secs, true, done, threads, elapsed[size_t(t)]);
+                    io_loop(cpart[size_t(t)], tick, secs, true, done, threads, elapsed[size_t(t)], !ref);
                 } catch (const std::exception& e) {
                     errors[size_t(threads + t)] = e.what();
                     done.fetch_add(1);
@@ -385,9 +406,12 @@ int main(int argc, char** argv)
         const uint64_t msgs = size ? total / size : 0;
         std::printf("{\"codec\": \"%s\", \"transport\": \"TCP 127.0.0.1 (epoll)\", \"clients\": %d, \"threads\": %d, "
                     "\"messages_in_flight\": %zu, \"size\": %zu, \"seconds\": %.3f, \"total_messages\": %llu, "
-                    "\"msg_per_s\": %.0f, \"MiB_per_s\": %.3f, \"latency_ns\": %.1f, \"payload_ok\": %s}\n",
+                    "\"msg_per_s\": %.0f, \"MiB_per_s\": %.3f, \"latency_ns\": %.1f, \"payload_ok\": %s, \"reads\": %llu, "
+                    "\"lane_requests\": %llu, \"lane_launches\": %llu, \"lane_state\": %d}\n",
                     codec.c_str(), clients, threads, messages, size, el, (unsigned long long)msgs, msgs / el,
-                    total / el / (1 << 20), msgs ? el * 1e9 / double(msgs) : 0.0, bad == 0 ? "true" : "false");
+                    total / el / (1 << 20), msgs ? el * 1e9 / double(msgs) : 0.0, bad == 0 ? "true" : "false",
+                    (unsigned long long)g_reads.load(), (unsigned long long)g_lane_requests.load(),
+                    (unsigned long long)g_lane_launches.load(), g_lane_state.load());
     } catch (const std::exception& e) {
         std::fprintf(stderr, "bench_echo_tcp: %s\n", e.what());
         return 3;
