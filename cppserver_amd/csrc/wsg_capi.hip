@@ -116,7 +116,7 @@ struct wsg_ctx {
     // through its mailboxes instead of a launch + synchronize ($WSG_LANE_MAX,
     // 0 = never)
     struct LaneServer* lane = nullptr;   // the device's (made on first use)
-    uint64_t lane_max = 64 << 10;
+    uint64_t lane_max = 512 << 10;
     uint32_t lane_groups = wsg::LANE_GROUPS_MAX;   // most frame groups of one request ($WSG_LANE_GROUPS)
     uint64_t lane_requests = 0;          // requests this context put on the lane (wsg_lane_stats)
     bool dead = false;                   // a lane request neither answered nor drained: buffers may still be written
@@ -540,20 +540,60 @@ LaneServer* lane_for(wsg_ctx* c)
     return c->lane->broken.load(std::memory_order_relaxed) ? nullptr : c->lane;
 }
 
-// Frame groups for a request of n frames: as many as the lane has idle
-// workgroups (W shared among the requests in flight), at most the context's
-// lane_groups, at least one per LANE_THREADS frames.  Returns the frames per
-// group; *groups = ceil(n / that).
-uint32_t lane_split(const wsg_ctx* c, const LaneServer* s, uint32_t n, uint32_t* groups)
+// A request's frame groups: runs of whole frames [f, f + cnt), each at most
+// LANE_THREADS frames over the byte range [lo, hi) of its boundaries b(f) ..
+// b(f + cnt) (b(0) = 0, b(n) = the request's end), about equal in bytes and
+// about as many as the lane has idle workgroups (W shared among the requests
+// in flight, at most the context's lane_groups).  A group's range is at most
+// `limit` bytes: strict (decode: the range is staged in LDS) a frame larger
+// than that does not fit the lane; otherwise (encode: the payload span is
+// staged when it fits, read in place when not) such a frame is a group alone.
+// Returns the group count; 0 when the request does not fit the lane (more
+// than LANE_GROUPS_MAX groups, or a frame too large for a strict stage).
+struct LaneGroup {
+    uint32_t f, cnt;
+    uint64_t lo, hi;
+};
+
+template <class Bound>
+uint32_t lane_plan(const wsg_ctx* c, const LaneServer* s, uint32_t n, uint64_t limit, bool strict, Bound b,
+                   LaneGroup* g)
 {
     const uint32_t busy = uint32_t(std::max(0, s->inflight.load(std::memory_order_relaxed))) + 1;
-    uint32_t g = std::max<uint32_t>(1, s->W / busy);
-    g = std::min(g, c->lane_groups);
-    g = std::max(g, (n + wsg::LANE_THREADS - 1) / wsg::LANE_THREADS);
-    g = std::max<uint32_t>(1, std::min(g, n));
-    const uint32_t per = (n + g - 1) / g;
-    *groups = (n + per - 1) / per;
-    return per;
+    const uint32_t want = std::max<uint32_t>(1, std::min(s->W / busy, c->lane_groups));
+    const uint64_t total = b(n);
+    const uint64_t target = std::max<uint64_t>(1, (total + want - 1) / want);
+    // b is non-decreasing: the first index in [a, z] whose bound is >= v (z if none)
+    const auto first_at_least = [&b](uint32_t a, uint32_t z, uint64_t v) {
+        while (a < z) {
+            const uint32_t m = a + (z - a) / 2;
+            if (b(m) >= v)
+                z = m;
+            else
+                a = m + 1;
+        }
+        return a;
+    };
+    uint32_t k = 0;
+    for (uint32_t f = 0; f < n;) {
+        if (k == wsg::LANE_GROUPS_MAX)
+            return 0;
+        const uint64_t lo = b(f);
+        if (strict && b(f + 1) - lo > limit)
+            return 0;
+        // the group ends at the first bound reaching the target, before the
+        // first past the limit, after at most LANE_THREADS frames, and holds
+        // at least one frame
+        const uint32_t z = uint32_t(std::min<uint64_t>(n, uint64_t(f) + wsg::LANE_THREADS));
+        const uint32_t e_target = first_at_least(f + 1, z, lo + target);
+        uint32_t e_limit = first_at_least(f + 1, z, lo + limit + 1);
+        if (b(e_limit) - lo > limit)
+            --e_limit;
+        const uint32_t e = std::max(f + 1, std::min(e_target, e_limit));
+        g[k++] = LaneGroup{f, e - f, lo, b(e)};
+        f = e;
+    }
+    return k;
 }
 
 // Requests of at most this many frames fit the lane (groups of at most
@@ -721,7 +761,7 @@ namespace {
 // wsg_create (no environment read on any data path).
 struct Knobs {
     bool check = false;             // $WSG_CHECK=1: checked launches (debug, see in_alloc)
-    uint64_t lane_max = 64 << 10;   // $WSG_LANE_MAX: largest lane request (0: the launch paths only)
+    uint64_t lane_max = 512 << 10;  // $WSG_LANE_MAX: largest lane request (0: the launch paths only; tools/lane_ab.py sweep)
     uint32_t lane_groups = wsg::LANE_GROUPS_MAX;   // $WSG_LANE_GROUPS: most frame groups per lane request
     uint64_t host_direct_max = 4 << 20;            // $WSG_HOST_DIRECT_MAX: host batches read in place up to this
     uint64_t seg_bytes = 32ull << 20;              // $WSG_STAGE_MB: segment of the staged host pipelines
@@ -1524,25 +1564,27 @@ int decode_host_direct(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, const
     wsg_recv_info* info_dev =
         in_host_block(info, uint64_t(n) * sizeof(wsg_recv_info)) ? info : sl.h_info;
     LaneServer* ls = nullptr;
-    if (wire_len <= std::min<uint64_t>(c->lane_max, wsg::LANE_STAGE - 64) && n > 0 && n <= kLaneMaxFrames &&
-        strictly_increasing(frame_start, n) && (ls = lane_for(c))) {
-        // a few KiB (an echo's read): the device's resident lane, no launch;
-        // group k's wire range from its first start (0 for the first) to the
-        // next group's (wire_len after the last)
-        uint32_t groups = 0;
-        const uint32_t per = lane_split(c, ls, n, &groups);
+    LaneGroup grp[wsg::LANE_GROUPS_MAX];
+    uint32_t groups = 0;
+    if (wire_len <= c->lane_max && n > 0 && n <= kLaneMaxFrames && strictly_increasing(frame_start, n) &&
+        (ls = lane_for(c)) &&
+        (groups = lane_plan(c, ls, n, wsg::LANE_STAGE - 64, true, [&](uint32_t i) -> uint64_t {
+             return i == 0 ? 0 : i < n ? std::min(frame_start[i], wire_len) : wire_len;
+         }, grp))) {
+        // an echo's read, up to a few MiB: the device's resident lane, no
+        // launch; group k's wire range from its first start (0 for the first)
+        // to the next group's (wire_len after the last), staged whole in LDS
         uint64_t w[wsg::LANE_GROUPS_MAX][wsg::LANE_WORDS];
         for (uint32_t k = 0; k < groups; ++k) {
-            const uint32_t f = k * per, cnt = std::min(per, n - f);
             w[k][0] = wsg::LANE_DECODE | (uint64_t(n) << 32);
             w[k][1] = reinterpret_cast<uint64_t>(wire);
             w[k][2] = wire_len;
             w[k][3] = reinterpret_cast<uint64_t>(fs_dev);
             w[k][4] = reinterpret_cast<uint64_t>(out);
             w[k][5] = reinterpret_cast<uint64_t>(info_dev);
-            w[k][6] = uint64_t(f) | (uint64_t(cnt) << 32);
-            w[k][7] = k == 0 ? 0 : std::min(frame_start[f], wire_len);
-            w[k][8] = f + cnt < n ? std::min(frame_start[f + cnt], wire_len) : wire_len;
+            w[k][6] = uint64_t(grp[k].f) | (uint64_t(grp[k].cnt) << 32);
+            w[k][7] = grp[k].lo;
+            w[k][8] = grp[k].hi;
         }
         uint64_t errs = 0;
         uint32_t answered = 0;
@@ -1765,10 +1807,15 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
                 desc_dev = sl.h_desc;
             }
             LaneServer* ls = nullptr;
-            if (wire_off[n] <= c->lane_max && n <= kLaneMaxFrames && (ls = lane_for(c))) {
-                // a few KiB (the replies of an echo's read): the device's
+            LaneGroup grp[wsg::LANE_GROUPS_MAX];
+            uint32_t groups = 0;
+            if (wire_off[n] <= c->lane_max && n <= kLaneMaxFrames && (ls = lane_for(c)) &&
+                (groups = lane_plan(c, ls, n, wsg::LANE_PSTAGE - 64, false,
+                                    [&](uint32_t i) -> uint64_t { return wire_off[i]; }, grp))) {
+                // the replies of an echo's read, up to a few MiB: the device's
                 // resident lane at the offsets computed above, no launch;
-                // group k's payload span for its staging
+                // groups of about equal wire bytes, each group's payload span
+                // for its staging
                 const uint64_t* off_dev = wire_off;
                 if (!in_host_block(wire_off, (uint64_t(n) + 1) * sizeof(uint64_t))) {
                     if (int rc = slot_reserve(sl, 0, uint64_t(n) + 1, false))
@@ -1776,11 +1823,9 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
                     std::memcpy(sl.h_fs, wire_off, (size_t(n) + 1) * sizeof(uint64_t));
                     off_dev = sl.h_fs;
                 }
-                uint32_t groups = 0;
-                const uint32_t per = lane_split(c, ls, n, &groups);
                 uint64_t w[wsg::LANE_GROUPS_MAX][wsg::LANE_WORDS];
                 for (uint32_t k = 0; k < groups; ++k) {
-                    const uint32_t f = k * per, cnt = std::min(per, n - f);
+                    const uint32_t f = grp[k].f, cnt = grp[k].cnt;
                     uint64_t lo = UINT64_MAX, hi = 0;
                     for (uint32_t i = f; i < f + cnt; ++i)
                         if (desc[i].len) {

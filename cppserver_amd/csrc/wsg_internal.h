@@ -112,7 +112,7 @@ hipError_t launch_test_spin(hipStream_t s, uint32_t us);
 enum : uint32_t { LANE_DECODE = 1, LANE_ENCODE = 2, LANE_XOR = 3, LANE_XOR_INLINE = 4 };
 constexpr uint64_t LANE_INLINE = 40;     // xor: payloads up to this size travel in the task (w[4..8])
 constexpr uint32_t LANE_THREADS = 1024;   // one workgroup; frames per group (lane per frame)
-constexpr uint64_t LANE_STAGE = 64 << 10;  // decode: wire bytes staged in LDS (the lane's batch limit)
+constexpr uint64_t LANE_STAGE = 64 << 10;  // decode: wire bytes staged in LDS (one group's range limit)
 constexpr uint64_t LANE_PSTAGE = 64 << 10; // encode: payload arena staged in LDS when its 16-B blocks fit
 // LDS of the lane (one layout per op, the larger sized):
 //   decode: staged wire | info blocks (32 B) | payload bounds (2 x 8 B), key (4 B), frame starts (8 B) per frame
@@ -137,7 +137,7 @@ struct alignas(16) LaneUnit {
 //           w[7], w[8] = the group's wire range [lo, hi): its first start (0
 //           for the first group) to the next group's (wire_len after the last),
 //           clamped to wire_len — bit-identical to k_decode there; the table
-//           strictly increasing (the caller checks), wire_len + 64 <= LANE_STAGE
+//           strictly increasing (the caller checks), hi - lo + 64 <= LANE_STAGE
 //   encode: w[1..4] = payload, desc, wire_off (n + 1, host-computed), wire;
 //           w[6] = f_lo | cnt << 32; w[7], w[8] = the group's payload span
 //           [lo, hi) ({0, 0}: none)

@@ -1526,7 +1526,7 @@ __device__ __forceinline__ void lane_encode(const uint8_t* __restrict__ payload,
 }
 
 // Decode of one frame group on the lane (frame table strictly increasing,
-// the wire at most LANE_STAGE - 64 bytes): the group's frame starts and its
+// the group's range at most LANE_STAGE - 64 bytes): the group's frame starts and its
 // wire range [lo, hi) — from its first frame's start (0 for the first group)
 // to the next group's (wire_len for the last) — plus the 32 bytes a header
 // read may look past hi, staged in one round trip; a lane per frame parses
@@ -1552,7 +1552,7 @@ __device__ __forceinline__ void lane_decode(const uint8_t* __restrict__ wire, ui
     const uint32_t t = threadIdx.x;
     const uint64_t sb = lo & ~uint64_t(CHUNK - 1);
     const uint64_t se = min(hi + 32, wire_len);
-    const uint64_t wblocks = se > sb ? (se - sb + CHUNK - 1) / CHUNK : 0;   // <= LANE_STAGE / CHUNK (host)
+    const uint64_t wblocks = se > sb ? (se - sb + CHUNK - 1) / CHUNK : 0;   // <= LANE_STAGE / CHUNK (host's groups)
     const auto block = [s_wire, sb](uint64_t a) { return s_wire[(a - sb) / CHUNK]; };
     uint64_t st = 0, nx = wire_len;
     if (t < cnt)

@@ -335,14 +335,17 @@ int wsg_timing_read(wsg_ctx* ctx, double* total_ms, uint64_t* launches, int rese
 int wsg_timing_minmax(wsg_ctx* ctx, double* min_ms, double* max_ms);
 
 /* ---- the host lane (measurement / test hook) ----------------------------- */
-/* Page-locked host batches of at most $WSG_LANE_MAX wire bytes (default 64
+/* Page-locked host batches of at most $WSG_LANE_MAX wire bytes (default 512
  * KiB) whose frame table is strictly increasing, and wsg_xor_host calls of at
- * most that many bytes, go to the device's resident lane instead of a launch
- * and a synchronize per call (the C1 echo's reads; the per-call path).  One
- * lane per device serves every context of the process: $WSG_LANE_WGS
- * workgroups (default 8) on a high-priority stream, a mailbox each in host
- * memory; a request is cut into at most $WSG_LANE_GROUPS frame groups (one
- * per idle workgroup).  A launch ends after $WSG_LANE_IDLE_US (default 2000)
+ * most that many bytes (and 64 KiB), go to the device's resident lane instead
+ * of a launch and a synchronize per call (the C1 echo's reads; the per-call
+ * path).  One lane per device serves every context of the process:
+ * $WSG_LANE_WGS workgroups (default 8) on a high-priority stream, a mailbox
+ * each in host memory; a request is cut into frame groups of about equal
+ * bytes (one per idle workgroup, at most $WSG_LANE_GROUPS), each a run of at
+ * most 1024 whole frames; a decode with a frame larger than a group's 64 KiB
+ * stage, or a request needing more than 32 groups, takes the launch path.
+ * A launch ends after $WSG_LANE_IDLE_US (default 2000)
  * without a task and after $WSG_LANE_YIELD_US (default 2000) of running (a
  * running kernel holds up calls that wait for the device to drain); the next
  * call launches it again.  A request unanswered for $WSG_LANE_TIMEOUT_MS

@@ -222,6 +222,61 @@ def test_lane_payload_arenas(lane):
             assert np.array_equal(wire, wire_o), (arena, mis)
 
 
+def _batch_of(rng, lens, mask=0.9):
+    n = len(lens)
+    desc, total = wl.ragged_desc(rng, np.asarray(lens))
+    desc["opcode"] = rng.choice(OPCODES, n)
+    desc["mask"] = rng.random(n) < mask
+    desc["status"] = np.where(rng.random(n) < 0.05, rng.integers(0, 70000, n), 0)
+    return wl.random_bytes(rng, total + 16), desc
+
+
+def test_lane_byte_groups_large_batches():
+    """Batches past one group's LDS stage (64 KiB) up to the lane's request
+    limit ($WSG_LANE_MAX: 512 KiB by default, 2 MiB here) are cut into groups of about equal
+    wire bytes, each a run of whole frames whose range fits the stage (decode)
+    or whose payload span usually does (encode): many echo-sized frames,
+    a few frames just under the stage, ragged mixes, and the cases that leave
+    the lane — a frame larger than the stage (decode; encode keeps it, a group
+    alone), more frames than the lane's groups hold, a batch over the limit.
+    Encode, decode out of place and in place, against the oracle; the lane's
+    request count shows which went to the lane."""
+    c = _codec(WSG_LANE_MAX=2 << 20)
+    try:
+        rng = np.random.default_rng(77)
+        cap = 4 << 20
+        pin_p, pin_w = ca.pinned_empty(cap), ca.pinned_empty(cap)
+        pin_in, pin_out = ca.pinned_empty(cap), ca.pinned_empty(cap)
+        stage = 65536
+        cases = {   # name: (payload lengths, encode on the lane, decode on the lane)
+            "echo frames 760 KB": (np.full(20000, 32), True, True),
+            "frames just under the stage": (np.full(30, stage - 200), True, True),
+            "ragged 1.2 MB": (rng.integers(0, 2000, 1200), True, True),
+            "1.9 MB of 1000 B frames": (np.full(1900, 1000), True, True),
+            "one frame over the stage": (np.concatenate([np.full(500, 40), [100000], np.full(500, 40)]), True, False),
+            "over the frame limit": (np.zeros(40000, np.int64), False, False),
+            "over the request limit": (np.full(3000, 1000), False, False),
+            "65 KB just over one group": (np.full(1700, 33), True, True),
+        }
+        for name, (lens, enc_lane, dec_lane) in cases.items():
+            payload, desc = _batch_of(rng, lens)
+            wire_o, off_o = oracle.encode_batch(payload, desc)
+            assert len(wire_o) <= cap and len(payload) <= cap
+            pin_p[: len(payload)] = payload
+            r0, _, _ = c.lane_stats()
+            rc, wire, off = c.encode_batch_host(pin_p[: len(payload)], desc, wire=pin_w)
+            assert rc == 0 and np.array_equal(off, off_o) and np.array_equal(wire, wire_o), name
+            r1, _, _ = c.lane_stats()
+            assert (r1 - r0 == 1) == enc_lane, (name, "encode", r1 - r0)
+            fs = off_o[:-1].copy()
+            _check_decode(c, pin_in, wire_o, fs, pin_out)
+            _check_decode(c, pin_in, wire_o, fs)
+            r2, _, _ = c.lane_stats()
+            assert (r2 - r1 == 2) == dec_lane and (r2 - r1) in (0, 2), (name, "decode", r2 - r1)
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("groups", [1, 3, 32])
 def test_lane_group_counts(groups):
     """A request is cut into frame groups ($WSG_LANE_GROUPS at most; one per
