@@ -277,6 +277,34 @@ def test_lane_byte_groups_large_batches():
         c.close()
 
 
+def test_launch_path_status_from_the_latch(launch):
+    """In-place decodes of 4096 frames or more on the launch path read the
+    error latch back and skip the status pass over the records when no frame
+    erred: clean batches, a truncated last frame, a frame running into the
+    next (ETRUNC turned EINVAL by the pass), a start past the wire, each
+    followed by a clean batch (the latch re-armed), against the oracle."""
+    rng = np.random.default_rng(31)
+    payload, desc = _batch_of(rng, rng.integers(0, 90, 6000))
+    wire_o, off_o = oracle.encode_batch(payload, desc)
+    fs = off_o[:-1].copy()
+    pin, pout = ca.pinned_empty(len(wire_o) + 64), ca.pinned_empty(len(wire_o) + 64)
+    bad = {
+        "truncated last": (wire_o[:-3], fs),
+        "runs into the next": (wire_o, np.sort(np.concatenate([fs, fs[3000:3001] + 1])).astype(np.uint64)),
+        "start past the wire": (wire_o, np.concatenate([fs, [len(wire_o) + 40]]).astype(np.uint64)),
+        "first frame's header garbage": (np.concatenate([np.full(2, 0x7F, np.uint8), wire_o[2:]]), fs),
+    }
+    for name, (w, f) in bad.items():
+        for ww, ff in ((wire_o, fs), (w, f), (wire_o, fs)):
+            rc_o, out_o, info_o = oracle.decode_batch(ww, ff)
+            pin[: len(ww)] = ww
+            rc, out, info = launch.decode_batch_host(pin[: len(ww)], ff, out=pout)
+            assert rc == rc_o, name
+            assert np.array_equal(out[: len(ww)], out_o), name
+            for fld in INFO_FIELDS:
+                assert np.array_equal(info[fld], info_o[fld]), (name, fld)
+
+
 @pytest.mark.parametrize("groups", [1, 3, 32])
 def test_lane_group_counts(groups):
     """A request is cut into frame groups ($WSG_LANE_GROUPS at most; one per
