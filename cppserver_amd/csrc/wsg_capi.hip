@@ -1728,7 +1728,16 @@ int wsg_decode_batch_host(wsg_ctx* c, const uint8_t* wire, uint64_t wire_len, co
                 return rc;
         // the pipeline's kernels latched into d_err_host (segment-relative frame
         // indices, meaningless to the caller); the status comes from the
-        // per-frame errors below, and the caller's own latch is left alone
+        // per-frame errors below, and the caller's own latch is left alone.
+        // Many frames: the latch (every kernel has finished: the slots have
+        // drained) read back first, and an untouched one skips the pass
+        if (n >= kLatchFrames) {
+            WSG_HIP(hipMemcpyAsync(c->h_err_copy, c->d_err_host, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                   c->stream));
+            WSG_HIP(hipStreamSynchronize(c->stream));
+            if (*c->h_err_copy == ~0ull)
+                return WSG_OK;
+        }
 
         // batch semantics: a frame that runs into the next segment's first frame
         // overlaps it (EINVAL), it is not truncated; and the status is the error

@@ -277,32 +277,56 @@ def test_lane_byte_groups_large_batches():
         c.close()
 
 
-def test_launch_path_status_from_the_latch(launch):
-    """In-place decodes of 4096 frames or more on the launch path read the
-    error latch back and skip the status pass over the records when no frame
-    erred: clean batches, a truncated last frame, a frame running into the
-    next (ETRUNC turned EINVAL by the pass), a start past the wire, each
-    followed by a clean batch (the latch re-armed), against the oracle."""
-    rng = np.random.default_rng(31)
-    payload, desc = _batch_of(rng, rng.integers(0, 90, 6000))
+def _latch_cases(rng, n):
+    payload, desc = _batch_of(rng, rng.integers(0, 90, n))
     wire_o, off_o = oracle.encode_batch(payload, desc)
     fs = off_o[:-1].copy()
-    pin, pout = ca.pinned_empty(len(wire_o) + 64), ca.pinned_empty(len(wire_o) + 64)
-    bad = {
+    mid = n // 2
+    return wire_o, fs, {
         "truncated last": (wire_o[:-3], fs),
-        "runs into the next": (wire_o, np.sort(np.concatenate([fs, fs[3000:3001] + 1])).astype(np.uint64)),
+        "runs into the next": (wire_o, np.sort(np.concatenate([fs, fs[mid:mid + 1] + 1])).astype(np.uint64)),
         "start past the wire": (wire_o, np.concatenate([fs, [len(wire_o) + 40]]).astype(np.uint64)),
         "first frame's header garbage": (np.concatenate([np.full(2, 0x7F, np.uint8), wire_o[2:]]), fs),
     }
+
+
+def _latch_check(c, name, ww, ff, pin=None, pout=None):
+    rc_o, out_o, info_o = oracle.decode_batch(ww, ff)
+    if pin is not None:   # page-locked: in place on the launch path
+        pin[: len(ww)] = ww
+        rc, out, info = c.decode_batch_host(pin[: len(ww)], ff, out=pout)
+    else:                 # pageable: the staged pipeline
+        rc, out, info = c.decode_batch_host(np.array(ww), ff)
+    assert rc == rc_o, name
+    assert np.array_equal(out[: len(ww)], out_o), name
+    for fld in INFO_FIELDS:
+        assert np.array_equal(info[fld], info_o[fld]), (name, fld)
+
+
+def test_launch_path_status_from_the_latch(launch):
+    """Decodes of 4096 frames or more read the error latch back and skip the
+    status pass over the records when no frame erred — in place on the
+    launch path (page-locked buffers) and through the staged pipeline
+    (pageable buffers, 1 MiB segments: the frames cut into four): clean
+    batches around a truncated last frame, a frame running into the next
+    (ETRUNC turned EINVAL by the pass), a start past the wire and a garbage
+    header (each followed by a clean batch: the latch re-armed), rc / bytes /
+    records against the oracle."""
+    rng = np.random.default_rng(31)
+    wire_o, fs, bad = _latch_cases(rng, 6000)
+    pin, pout = ca.pinned_empty(len(wire_o) + 64), ca.pinned_empty(len(wire_o) + 64)
     for name, (w, f) in bad.items():
         for ww, ff in ((wire_o, fs), (w, f), (wire_o, fs)):
-            rc_o, out_o, info_o = oracle.decode_batch(ww, ff)
-            pin[: len(ww)] = ww
-            rc, out, info = launch.decode_batch_host(pin[: len(ww)], ff, out=pout)
-            assert rc == rc_o, name
-            assert np.array_equal(out[: len(ww)], out_o), name
-            for fld in INFO_FIELDS:
-                assert np.array_equal(info[fld], info_o[fld]), (name, fld)
+            _latch_check(launch, name, ww, ff, pin, pout)
+    staged = _codec(WSG_STAGE_MB=1)
+    try:
+        wire_o, fs, bad = _latch_cases(rng, 70000)
+        assert len(wire_o) > 3 << 20
+        for name, (w, f) in bad.items():
+            for ww, ff in ((wire_o, fs), (w, f), (wire_o, fs)):
+                _latch_check(staged, name, ww, ff)
+    finally:
+        staged.close()
 
 
 @pytest.mark.parametrize("groups", [1, 3, 32])

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build an A/B variant of libwsg.so with extra -D flags into cppserver_amd/_build/var/<name>/.
-#   tools/build_variant.sh NAME [-DFOO=1 ...]     ($KSRC: another wsg_kernels.hip, e.g. an older revision)
+#   tools/build_variant.sh NAME [-DFOO=1 ...]     ($KSRC / $CSRC: another wsg_kernels.hip / wsg_capi.hip, e.g. an older revision)
 set -e
 name=$1; shift
 root=$(cd "$(dirname "$0")/.." && pwd)
@@ -10,7 +10,7 @@ cd "$out"
 H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$root/include $*"
 $H $F -I$root/cppserver_amd/csrc -c ${KSRC:-$root/cppserver_amd/csrc/wsg_kernels.hip} -o k.o
-$H $F -c $root/cppserver_amd/csrc/wsg_capi.hip -o c.o
+$H $F -I$root/cppserver_amd/csrc -c ${CSRC:-$root/cppserver_amd/csrc/wsg_capi.hip} -o c.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws.cpp -o w.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws_api.cpp -o a.o
 $H -O3 -std=c++17 -fPIC -I$root/include -c $root/cppserver_amd/csrc/ws_batch.cpp -o b.o
