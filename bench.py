@@ -577,6 +577,37 @@ def pcie_inclusive(w, reps=3):
     return res
 
 
+def gpu_node_cpus(device_index=0):
+    """The NUMA node the GPU hangs off (its PCI function's numa_node in sysfs)
+    and that node's CPUs this process may use: (node, cpus) or (None, None).
+    The host-side legs run there, as a deployment binds its IO threads to the
+    GPU's node (numactl --cpunodebind): on the dual-socket GPU box a thread on
+    the other socket crosses the socket link for every mailbox poll (the
+    per-call echo 161 K vs 176 K msg/s, profiles/r5/numa_per_call_r5aa.log)."""
+    try:
+        import torch
+
+        p = torch.cuda.get_device_properties(device_index)
+        dev = "/sys/bus/pci/devices/%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        with open(os.path.join(dev, "numa_node")) as f:
+            node = int(f.read().strip())
+        if node < 0:
+            return None, None
+        with open("/sys/devices/system/node/node%d/cpulist" % node) as f:
+            spec = f.read().strip()
+        cpus = set()
+        for part in spec.split(","):
+            if "-" in part:
+                a, b = part.split("-")
+                cpus.update(range(int(a), int(b) + 1))
+            elif part:
+                cpus.add(int(part))
+        cpus &= os.sched_getaffinity(0)
+        return (node, cpus) if cpus else (None, None)
+    except Exception:   # noqa: BLE001  (no sysfs entry: the legs run unbound)
+        return None, None
+
+
 def _run_leg(cmd, timeout, env=None):
     """A host-side leg's child process; a time-out is reported in the line
     (returncode 124) rather than ending the bench.  env: variables added to
@@ -1575,15 +1606,28 @@ def main():
     # per second takes minutes; the GPU legs above are unchanged by it)
     host_legs = os.environ.get("WSG_BENCH_HOST_LEGS", "1") != "0"
     if rank == 0 and world == 1 and not args.no_extras and headline_cfg == "c2" and host_legs:
-        sb = session_batch_leg()
-        if sb is not None:
-            extras["session_batch"] = sb
-        c1 = echo_c1_leg()
-        if c1 is not None:
-            extras["echo_c1"] = c1
-        mc = multicast_leg()
-        if mc is not None:
-            extras["ws_multicast"] = mc
+        # the legs' processes on the GPU's NUMA node (inherited affinity;
+        # the reference-algorithm legs alike), this thread's mask restored after
+        node, cpus = gpu_node_cpus(local)
+        mask = os.sched_getaffinity(0)
+        if cpus:
+            os.sched_setaffinity(0, cpus)
+        try:
+            sb = session_batch_leg()
+            if sb is not None:
+                extras["session_batch"] = sb
+            c1 = echo_c1_leg()
+            if c1 is not None:
+                extras["echo_c1"] = c1
+            mc = multicast_leg()
+            if mc is not None:
+                extras["ws_multicast"] = mc
+        finally:
+            if cpus:
+                os.sched_setaffinity(0, mask)
+        extras["host_legs_cpus"] = {"numa_node": node, "cpus": len(cpus) if cpus else None,
+                                    "what": "session / echo / multicast legs bound to the GPU's NUMA node "
+                                            "(both the drop-in and the reference-algorithm legs)"}
     if cpu is not None:
         run_deferred_cpu_baselines(cpu)
     cpu1, cpu_mt = headline_cpu.get("cpu_baseline"), headline_cpu.get("cpu_baseline_mt")
