@@ -7,7 +7,9 @@ goes through the device encode (piece or small-frame kernel, whichever the
 batch selects) and decode, out of place and in place, and through the
 host-staged pair (pageable buffers: the staged pipeline; page-locked
 buffers: the direct path of small batches); bytes, offsets, per-frame fields and status must equal the
-oracle's.  Bit-exact, no tolerance.  $WSG_FUZZ_SEEDS widens the run."""
+oracle's; every third batch is also decoded with a few wire bytes
+overwritten or the wire cut short.  Bit-exact, no tolerance.
+$WSG_FUZZ_SEEDS widens the run."""
 import os
 
 import numpy as np
@@ -88,6 +90,28 @@ def test_fuzz_encode_decode_vs_oracle(codec, seed):
     assert rc_h == rc_o and np.array_equal(out_h, out_o)
     for f in INFO_FIELDS:
         assert np.array_equal(info_h[f], info_o[f]), f
+    # every third seed: a few wire bytes overwritten (headers broken, lengths
+    # running into the next frame or past the wire) or the wire cut short,
+    # the same frame table: status, bytes and records through the device
+    # decode and both host paths (the lane, the launch path's latch, the
+    # staged pipeline) against the oracle
+    if seed % 3 == 0 and len(wire_o):
+        rng = np.random.default_rng(7000 + seed)
+        bad = wire_o.copy()
+        for q in rng.integers(0, len(bad), int(rng.integers(1, 4))):
+            bad[q] = rng.integers(0, 256)
+        if rng.random() < 0.3:
+            bad = bad[: int(rng.integers(0, len(bad)))]
+        rc_b, out_b, info_b = oracle.decode_batch(bad, fs)
+        got = [gpu_decode(codec, bad, fs, inplace=False), codec.decode_batch_host(bad, fs)]
+        if len(bad):
+            pin_in[: len(bad)] = bad
+            got.append(codec.decode_batch_host(pin_in[: len(bad)], fs, out=pin_out))
+        for rc_g, out_g, info_g in got:
+            assert rc_g == rc_b
+            assert np.array_equal(out_g[: len(bad)], out_b)
+            for f in INFO_FIELDS:
+                assert np.array_equal(info_g[f], info_b[f]), f
 
 
 @pytest.mark.parametrize("seed", range(int(os.environ.get("WSG_FUZZ_SEEDS", 60))))
