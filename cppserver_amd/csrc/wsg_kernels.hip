@@ -1657,14 +1657,24 @@ __device__ __forceinline__ void lane_xor(uint8_t* buf, uint64_t len, uint32_t ke
 // request's PCIe reads and writes spread over as many CUs as it has groups
 // (one CU has few requests in flight: one workgroup took ~5 us to stage a 38
 // KB read and ~7 us to write it back, round 4).
-__global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ bell, uint64_t idle_ticks,
+// The lane's workgroups on the XCDs nearest the PCIe root: block b runs on
+// XCC b mod 8 (round-robin dispatch), and a poller on XCCs 0-3 reaches
+// page-locked host memory ~0.2 us sooner per round trip than one on 4-7
+// (tools/xcd_probe.hip).  Blocks on the other XCCs leave at once; workgroup g
+// of the lane is block (g / LANE_NEAR_XCCS) * 8 + g % LANE_NEAR_XCCS.
+constexpr uint32_t LANE_XCCS = 8, LANE_NEAR_XCCS = 4;
+
+__global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ bell, uint32_t W, uint64_t idle_ticks,
                                                        uint64_t yield_ticks, uint32_t gen, uint64_t delay_ticks)
 {
     __shared__ uint64_t s_w[LANE_WORDS];
     __shared__ int s_go;         // 1: a task in s_w; 0: leave
     __shared__ uint32_t s_err;   // the task's frames with an error (decode)
     __shared__ v4u s_mem[LANE_LDS / 16];   // the op's staging (lane_decode / lane_encode layouts)
-    const uint32_t t = threadIdx.x, g = blockIdx.x, W = gridDim.x;
+    const uint32_t t = threadIdx.x;
+    const uint32_t x = blockIdx.x % LANE_XCCS, g = blockIdx.x / LANE_XCCS * LANE_NEAR_XCCS + x;
+    if (x >= LANE_NEAR_XCCS || g >= W)
+        return;   // (a block-uniform exit before any barrier or memory access)
     uint64_t j = 0;     // (wave 0) this workgroup's mailbox position: ticket g + j W
     uint32_t why = 0;   // (wave 0) why it leaves: 1 idle or yield (announced in `closing`), 2 stop, 3 closing seen
     const LaneTask* box = bell->box[g];
@@ -2362,7 +2372,8 @@ hipError_t launch_lane(hipStream_t s, LaneBell* bell, uint32_t workgroups, uint6
 {
     if (workgroups < 1 || workgroups > LANE_WGS_MAX || gen == 0)
         return hipErrorInvalidValue;
-    k_lane<<<workgroups, LANE_THREADS, 0, s>>>(bell, idle_ticks, yield_ticks, gen, delay_ticks);
+    const uint32_t blocks = (workgroups + LANE_NEAR_XCCS - 1) / LANE_NEAR_XCCS * LANE_XCCS;
+    k_lane<<<blocks, LANE_THREADS, 0, s>>>(bell, workgroups, idle_ticks, yield_ticks, gen, delay_ticks);
     return hipGetLastError();
 }
 
