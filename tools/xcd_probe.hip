@@ -5,15 +5,18 @@
 // serves a ping-pong: the host writes a sequence number into page-locked
 // memory, the wave polls it and answers with a vector store, the host spins
 // on the answer.  For which = 0 .. BLOCKS-1: the XCC id and the median /
-// p10 / p90 round trip, one JSON line each.  The wave always ends: a stop
-// value, and a wall-clock limit.
-//   xcd_probe [BLOCKS=16] [ROUNDS=20000]
+// p10 / p90 round trip, one JSON line each.  With NOISE > 0, block 0 serves
+// and blocks 1 .. NOISE poll page-locked words of their own the same way
+// (pollers that never get a task: does their traffic slow the server?).
+// The waves always end: a stop value, and a wall-clock limit.
+//   xcd_probe [BLOCKS=16] [ROUNDS=20000] [NOISE=0]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x)                                                                                  \
@@ -31,8 +34,24 @@ namespace {
 __device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xF; }
 
 __global__ __launch_bounds__(64) void k_worker(const uint64_t* bell, uint64_t* ans, uint64_t* where, uint32_t which,
-                                               uint64_t ticks)
+                                               uint32_t noise, uint64_t ticks)
 {
+    if (noise && blockIdx.x >= 1 && blockIdx.x <= noise) {
+        // a poller without tasks: its own word (one 4 KiB page apart), until
+        // the server's bell says stop or the wall-clock limit
+        const uint64_t* mine = bell + 512 * blockIdx.x;
+        const uint64_t t0 = wall_clock64();
+        for (uint32_t it = 0; it < (1u << 30); ++it) {
+            const uint64_t v = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) |
+                               __hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (v == ~uint64_t(0))
+                break;
+            if ((it & 63) == 63 && wall_clock64() - t0 > 4 * ticks)
+                break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        return;
+    }
     if (blockIdx.x != which)
         return;
     if (threadIdx.x == 0)
@@ -62,22 +81,25 @@ int main(int argc, char** argv)
 {
     const uint32_t blocks = argc > 1 ? uint32_t(std::atoi(argv[1])) : 16;
     const int rounds = argc > 2 ? std::atoi(argv[2]) : 20000;
+    const uint32_t noise = argc > 3 ? uint32_t(std::atoi(argv[3])) : 0;
     CK(hipSetDevice(0));
     int khz = 0;
     CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0));
     const uint64_t ticks = uint64_t(khz) * 1000;   // 1 s without a ring: the wave leaves
     uint64_t* h = nullptr;
-    CK(hipHostMalloc(&h, 4096, hipHostMallocMapped | hipHostMallocCoherent));
+    CK(hipHostMalloc(&h, 4096 * 64, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(h, 0, 4096 * 64);
     volatile uint64_t* bell = h;
     uint64_t* ans = h + 64;
     uint64_t* where = h + 128;
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    for (uint32_t which = 0; which < blocks; ++which) {
+    for (uint32_t which = 0; which < (noise ? 1u : blocks); ++which) {
         *bell = 0;
         __atomic_store_n(ans, 0, __ATOMIC_SEQ_CST);
         __atomic_store_n(where, 0, __ATOMIC_SEQ_CST);
-        hipLaunchKernelGGL(k_worker, dim3(blocks), dim3(64), 0, s, h, ans, where, which, ticks);
+        hipLaunchKernelGGL(k_worker, dim3(std::max(blocks, noise + 1)), dim3(64), 0, s, h, ans, where, which, noise,
+                           ticks);
         CK(hipGetLastError());
         std::vector<double> v;
         bool ok = true;
@@ -108,9 +130,9 @@ int main(int argc, char** argv)
         if (v.empty())
             std::printf("{\"block\": %u, \"xcc\": %lld, \"ok\": false}\n", which, (long long)w - 1);
         else
-            std::printf("{\"block\": %u, \"xcc\": %lld, \"us_median\": %.3f, \"us_p10\": %.3f, \"us_p90\": %.3f, "
-                        "\"ok\": %s}\n",
-                        which, (long long)w - 1, v[v.size() / 2], v[v.size() / 10], v[v.size() * 9 / 10],
+            std::printf("{\"block\": %u, \"xcc\": %lld, \"noise\": %u, \"us_median\": %.3f, \"us_p10\": %.3f, "
+                        "\"us_p90\": %.3f, \"ok\": %s}\n",
+                        which, (long long)w - 1, noise, v[v.size() / 2], v[v.size() / 10], v[v.size() * 9 / 10],
                         ok ? "true" : "false");
         std::fflush(stdout);
     }
