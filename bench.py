@@ -141,6 +141,10 @@ def dist_setup(args):
         share = backend != "nccl" or os.environ.get("WSG_BENCH_SHARE_DEVICES") == "1"
         if share:
             local = local % torch.cuda.device_count()
+        elif local >= torch.cuda.device_count():
+            print("bench.py: --gpus %d needs a GPU per rank, %d visible (WSG_BENCH_SHARE_DEVICES=1 lets ranks "
+                  "share them for a rehearsal)" % (world, torch.cuda.device_count()), file=sys.stderr, flush=True)
+            sys.exit(2)
         if backend == "nccl" and share:
             # RCCL over ranks sharing a GPU (a rehearsal on a smaller box): a host
             # id per rank makes RCCL see one GPU per host and connect the ranks
