@@ -135,17 +135,16 @@ def dist_setup(args):
     if world > 1:
         import torch.distributed as dist
 
-        # $WSG_BENCH_BACKEND=gloo rehearses the N-rank path on fewer GPUs
-        # (ranks share devices round-robin); the real run is RCCL, one GPU per rank
-        backend = os.environ.get("WSG_BENCH_BACKEND", "nccl")
-        share = backend != "nccl" or os.environ.get("WSG_BENCH_SHARE_DEVICES") == "1"
+        # $WSG_BENCH_SHARE_DEVICES=1 rehearses the N-rank path on fewer GPUs
+        # (ranks share devices round-robin); the real run is one GPU per rank
+        share = os.environ.get("WSG_BENCH_SHARE_DEVICES") == "1"
         if share:
             local = local % torch.cuda.device_count()
         elif local >= torch.cuda.device_count():
             print("bench.py: --gpus %d needs a GPU per rank, %d visible (WSG_BENCH_SHARE_DEVICES=1 lets ranks "
                   "share them for a rehearsal)" % (world, torch.cuda.device_count()), file=sys.stderr, flush=True)
             sys.exit(2)
-        if backend == "nccl" and share:
+        if share:
             # RCCL over ranks sharing a GPU (a rehearsal on a smaller box): a host
             # id per rank makes RCCL see one GPU per host and connect the ranks
             # through its socket transport (it refuses two ranks of one host on
@@ -154,20 +153,29 @@ def dist_setup(args):
             os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
             os.environ.setdefault("NCCL_IB_DISABLE", "1")
         torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-            # a host-side group for waits that must not park an RCCL kernel on
-            # the GPUs (c5_capi_leg: a child process drives every GPU meanwhile)
-            global CPU_GROUP
-            CPU_GROUP = dist.new_group(backend="gloo")
-        else:
-            dist.init_process_group(backend)
+        # The bench's own group is gloo: barriers, max over ranks and the
+        # product's RCCL id travel over host sockets, so the only RCCL in a
+        # rank is the one the product library loads (wsg_mgpu_create_rank) —
+        # not torch's bundled RCCL beside it.  torch's RCCL is set up only for
+        # the cross-check asked for with $WSG_BENCH_TORCH_GATHER=1 (rccl_group).
+        dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(local)
     return rank, world, local
 
 
-CPU_GROUP = None
+_RCCL_GROUP = None
+
+
+def rccl_group():
+    """torch.distributed's own RCCL group, made on first use (every rank
+    calls it): only the labelled torch-gather cross-check uses it."""
+    global _RCCL_GROUP
+    if _RCCL_GROUP is None:
+        import torch.distributed as dist
+
+        _RCCL_GROUP = dist.new_group(backend="nccl")
+    return _RCCL_GROUP
 
 
 def barrier(world, group=None):
@@ -177,13 +185,15 @@ def barrier(world, group=None):
         dist.barrier(group=group)
 
 
-def max_over_ranks(x, world, device):
+def max_over_ranks(x, world, device=None):
+    """The max of a host scalar over the ranks (over the gloo group: no
+    device collective)."""
     if world == 1:
         return x
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -870,12 +880,10 @@ def fanout_graph_leg(w, per_graph=20, replays=10):
             "GiBps": round(w.payload_bytes / (us * 1e-6) / GIB, 1)}
 
 
-def _gather_tensors(wire, woff):
-    """Device tensors for RCCL; host copies when the group is gloo (the
-    $WSG_BENCH_BACKEND=gloo rehearsal of N ranks on fewer GPUs)."""
-    import torch.distributed as dist
-
-    if dist.get_backend() == "gloo":
+def _gather_tensors(wire, woff, group):
+    """Device tensors for an RCCL group; host copies for the bench's own
+    gloo group."""
+    if group is None:
         n = int(woff[-1].item())
         return wire[:n].cpu(), woff.cpu()
     return wire, woff
@@ -899,34 +907,6 @@ def gather_root_check(parts, n_total, size, chunk=1024):
         ref, _ = oracle.encode_batch(wl.c5_payload_np(ids, size), wl.c5_desc(ids, size))
         ok &= bool(np.array_equal(job[g * fsz: (g + 1) * fsz].cpu().numpy(), ref))
     return bool(ok), int(job_off[-1].item())
-
-
-def gather_leg(w, world, rank, device):
-    """C5's exchange step: every rank's framed output to rank 0 over RCCL
-    (torch.distributed's group: variable-size grouped send/recv,
-    cppserver_amd.shard.gather_frames), timed once after the encode steps
-    (max over ranks); the root reassembles and checks sampled frames."""
-    import torch
-
-    from cppserver_amd import shard
-
-    torch.cuda.synchronize()
-    barrier(world)
-    t0 = time.perf_counter()
-    parts = shard.gather_frames(*_gather_tensors(w.wire, w.woff))
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    barrier(world)
-    dt = max_over_ranks(dt, world, device)
-    res = {"ms": round(dt * 1e3, 3)}
-    if parts is not None:
-        moved = sum(int(p[1][-1].item()) for r, p in enumerate(parts) if r != 0)
-        ids, desc, size = w.host
-        n_total = sum(int(p[1].numel()) - 1 for p in parts)
-        ok, total = gather_root_check(parts, n_total, size)
-        res.update({"bytes_into_root": moved, "GBps_into_root": round(moved / dt / 1e9, 1), "job_bytes": total,
-                    "root_check": ok})
-    return res
 
 
 def c5_rank_leg(world, rank, local, device, n_total=1 << 20, size=16384, chunk=1024, reps=3):
@@ -953,7 +933,7 @@ def c5_rank_leg(world, rank, local, device, n_total=1 << 20, size=16384, chunk=1
     from cppserver_amd import shard
     from cppserver_amd import workloads as wl
 
-    group = CPU_GROUP if CPU_GROUP is not None else dist.group.WORLD
+    group = None   # (the bench's gloo group: the id travels over host sockets)
     obj = [ca.MultiGPU.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0, group=group)
     g = ca.MultiGPU.rank(local, obj[0], rank, world)
@@ -1063,7 +1043,7 @@ def c5_job_leg(world, rank, device, codec, n_total=1 << 20, size=16384, chunk=10
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
-    parts = shard.gather_frames(*_gather_tensors(wire, woff))
+    parts = shard.gather_frames(*_gather_tensors(wire, woff, rccl_group()), group=rccl_group())
     torch.cuda.synchronize()
     dt = max_over_ranks(time.perf_counter() - t0, world, device)
     res = {"workload": "C5: %d x %d B frames round-robin (chunks of %d) over %d GPUs, gather to rank 0"
@@ -1143,7 +1123,7 @@ def c5_capi_leg(world, rank, n_total=1 << 20, timeout=300):
     res = None
     if rank == 0:
         env = dict(os.environ)
-        if os.environ.get("WSG_BENCH_SHARE_DEVICES") == "1" or os.environ.get("WSG_BENCH_BACKEND", "nccl") != "nccl":
+        if os.environ.get("WSG_BENCH_SHARE_DEVICES") == "1":
             env["WSG_MGPU_ONE_DEVICE"] = "1"   # the rehearsal's ranks share a GPU: so do the tool's
         try:
             r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mgpu_c5.py"), str(world), str(n_total)],
@@ -1154,7 +1134,7 @@ def c5_capi_leg(world, rank, n_total=1 << 20, timeout=300):
                 res = {"error": (r.stderr or r.stdout).strip()[-300:]}
         except subprocess.TimeoutExpired:
             res = {"error": "no result within %d s" % timeout}
-    barrier(world, CPU_GROUP)
+    barrier(world)
     return res
 
 
@@ -1547,7 +1527,12 @@ def main():
               "region_host": {"submit_ms": round(r["submit_ms"], 4),
                               "wall_minus_events_ms": round(elapsed * 1e3 - r["region_event_ms"], 4)}}
     if w.cfg == "c5" and world > 1:
-        extras["gather"] = gather_leg(w, world, rank, device)
+        # the exchange step: the job's shards encoded and gathered to rank 0
+        # by the product's rank form (RCCL inside the library)
+        try:
+            extras["c5_job"] = c5_rank_leg(world, rank, local, device)
+        except Exception as e:   # noqa: BLE001
+            extras["c5_job"] = {"error": repr(e)[:300]}
     if w.cfg == "c2" and world > 1 and not args.no_extras:
         try:
             extras["pcie_inclusive_all_ranks"] = pcie_all_ranks_leg(w, world, rank, device)
@@ -1563,18 +1548,20 @@ def main():
         except Exception as e:   # noqa: BLE001
             extras["c5_job"] = {"error": repr(e)[:300]}
         torch.cuda.empty_cache()
-        if os.environ.get("WSG_BENCH_TORCH_GATHER", "1") != "0":
-            # labelled cross-check: the same job gathered by torch.distributed
-            try:
-                extras["c5_job_torch_crosscheck"] = c5_job_leg(world, rank, device, codec, n_total=c5_frames)
-            except Exception as e:   # noqa: BLE001
-                extras["c5_job_torch_crosscheck"] = {"error": repr(e)[:300]}
         if os.environ.get("WSG_BENCH_CAPI_RCCL", "1") != "0":
             # the one-process form of the same entry (wsg_mgpu_create over all
             # N GPUs, device / xGMI peer copies), in a child process
             capi = c5_capi_leg(world, rank, n_total=c5_frames)
             if capi is not None:
                 extras["c5_job_one_process"] = capi
+        if os.environ.get("WSG_BENCH_TORCH_GATHER") == "1":
+            # labelled cross-check, only when asked and after the product's
+            # legs: the same job gathered by torch.distributed's own RCCL
+            # (a second RCCL stack in the rank from here on)
+            try:
+                extras["c5_job_torch_crosscheck"] = c5_job_leg(world, rank, device, codec, n_total=c5_frames)
+            except Exception as e:   # noqa: BLE001
+                extras["c5_job_torch_crosscheck"] = {"error": repr(e)[:300]}
     cpu = host_cpu() if (rank == 0 and world == 1 and not args.no_cpu) else None
     headline_cpu = {}
     if cpu is not None:
@@ -1639,7 +1626,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        okt = torch.tensor([1 if ok else 0], device=device)
+        okt = torch.tensor([1 if ok else 0])
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok = bool(okt.item())
 

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <thread>
+#include <unordered_set>
 
 namespace CppServer {
 namespace WS {
@@ -582,6 +583,7 @@ void WSServer::RemoveSession(const std::shared_ptr<WSSession>& session)
 
 void WSServer::EnableBatchReceive(bool on)
 {
+    std::lock_guard<std::recursive_mutex> one(_rx_switch);
     std::unique_lock<std::shared_mutex> locker(_sessions_lock);
     if (on == (_rx_batch != nullptr))
         return;
@@ -589,8 +591,29 @@ void WSServer::EnableBatchReceive(bool on)
         _rx_batch = std::make_shared<WSReceiveBatch>(nullptr);   // flushes decode on the flushing thread's codec
         if (!_batch_devices.empty())
             _rx_batch->SetDevices(_batch_devices);
-        for (auto& s : _sessions)
-            s->SetReceiveBatch(_rx_batch.get());
+        const std::shared_ptr<WSReceiveBatch> batch = _rx_batch;
+        const auto sessions = _sessions;
+        locker.unlock();
+        // outside the sessions lock: a session leaving a batch of its own
+        // delivers the frames it queued there, and their callbacks may call
+        // Multicast or sessions() (sessions added meanwhile got the batch
+        // from AddSession)
+        for (auto& s : sessions)
+            s->SetReceiveBatch(batch.get());
+        // a session removed meanwhile may have been attached after
+        // RemoveSession detached it: detach it again
+        std::vector<std::shared_ptr<WSSession>> removed;
+        {
+            std::shared_lock<std::shared_mutex> still(_sessions_lock);
+            std::unordered_set<const WSSession*> live;
+            for (auto& s : _sessions)
+                live.insert(s.get());
+            for (auto& s : sessions)
+                if (!live.count(s.get()))
+                    removed.push_back(s);
+        }
+        for (auto& s : removed)
+            s->SwapReceiveBatch(nullptr, false);
         return;
     }
     // detach outside the sessions lock (see RemoveSession); a flush in

@@ -204,6 +204,10 @@ void WSReceiveBatch::Clear(WebSocket& ws)
 
 void WSReceiveBatch::Forget(WebSocket& ws)
 {
+    if (std::vector<Rec>* d = DrainRecs())   // from a callback of a Drain's delivery on this thread
+        for (Rec& r : *d)
+            if (r.ws == &ws)
+                r.ws = nullptr;
     std::unique_lock<QueueLock> locker(_lock);
     for (Rec& r : _cur.recs)
         if (r.ws == &ws)
@@ -235,25 +239,126 @@ void WSReceiveBatch::Forget(WebSocket& ws)
     _waiters.fetch_sub(1, std::memory_order_relaxed);
 }
 
+namespace {
+template <class Recs>
+bool holds(const Recs& recs, size_t from, const WebSocket* ws)
+{
+    for (size_t r = from; r < recs.size(); ++r)
+        if (recs[r].ws == ws)
+            return true;
+    return false;
+}
+} // namespace
+
+std::vector<WSReceiveBatch::Rec>*& WSReceiveBatch::DrainRecs()
+{
+    static thread_local std::vector<Rec>* recs = nullptr;
+    return recs;
+}
+
 void WSReceiveBatch::Drain(WebSocket& ws)
 {
+    // Only ws's own frames are waited for, never the rest of another
+    // thread's flush: two threads whose callbacks each move a connection off
+    // the batch the other is flushing must not block on each other.
+    Batch mine;   // ws's queued frames, taken out while another thread flushes
     for (;;) {
-        {
-            std::scoped_lock locker(_lock);
-            if (_flushing && _flusher == std::this_thread::get_id())
-                return;   // (a callback of this thread's flush: the rest goes with a later flush)
-            bool queued = false;
-            for (const Rec& r : _cur.recs)
-                if (r.ws == &ws) {
-                    queued = true;
-                    break;
-                }
-            if (!queued && !_flushing)
-                return;
+        std::unique_lock<QueueLock> locker(_lock);
+        if (_flushing && _flusher == std::this_thread::get_id())
+            return;   // (a callback of this thread's flush: the rest goes with a later flush)
+        if (_flushing) {
+            // ws's frames still ahead of (or at) the record the other flush
+            // delivers: wait for it to move past them (it announces every
+            // change of connection, _pos before _waiters, as for Forget)
+            _waiters.fetch_add(1, std::memory_order_seq_cst);
+            _busy_cv.wait(locker, [&] {
+                return !_flushing || !holds(_spare.recs, _pos.load(std::memory_order_seq_cst), &ws);
+            });
+            _waiters.fetch_sub(1, std::memory_order_relaxed);
         }
-        if (Flush() == 0)
-            std::this_thread::yield();   // another thread's flush is delivering: wait for it to end
+        if (!holds(_cur.recs, 0, &ws))
+            return;
+        if (!_flushing) {
+            locker.unlock();
+            Flush();   // (0 when another thread started one meanwhile: again)
+            continue;
+        }
+        // Another flush runs: ws's queued frames leave the queue and are
+        // unmasked and delivered here, in their order; ws's earlier frames
+        // have all been delivered (above) and no later one is queued while
+        // its connection drains (RouteFrames waits).
+        for (Rec& r : _cur.recs) {
+            if (r.ws != &ws)
+                continue;
+            Rec m = r;
+            r.ws = nullptr;
+            if (r.frame >= 0) {
+                const size_t f = size_t(r.frame);
+                const uint64_t at = _cur.fs[f];
+                const uint64_t end = f + 1 < _cur.fs.size() ? _cur.fs[f + 1] : _cur.wire.len;
+                const uint8_t* frame = _cur.wire.p + at;
+                Grow(mine.wire, mine.wire.len + (end - at));
+                std::memcpy(mine.wire.p + mine.wire.len, frame, end - at);
+                if ((frame[1] & 0x80) && (frame[r.hdr - 4] | frame[r.hdr - 3] | frame[r.hdr - 2] | frame[r.hdr - 1]))
+                    mine.keyed = true;
+                m.frame = int64_t(mine.fs.size());
+                mine.fs.push_back(mine.wire.len);
+                mine.wire.len += end - at;
+            }
+            mine.recs.push_back(m);
+        }
+        break;
     }
+    struct Free {
+        Batch& b;
+        std::vector<Rec>* outer;   // (a Drain from a callback of another Drain's delivery)
+        ~Free()
+        {
+            DrainRecs() = outer;
+            Release(b.wire);
+            Release(b.out);
+        }
+    } free_mine{mine, DrainRecs()};
+    const uint8_t* base = Unmask(mine);
+    DrainRecs() = &mine.recs;   // (a Forget(ws) from one of these callbacks drops the rest)
+    for (size_t r = 0; r < mine.recs.size(); ++r) {
+        const Rec rec = mine.recs[r];
+        if (!rec.ws)
+            continue;
+        if (rec.frame < 0) {
+            rec.ws->ResetMessage();
+            continue;
+        }
+        const size_t f = size_t(rec.frame);
+        const uint64_t at = mine.fs[f] + rec.hdr;
+        const uint64_t end = f + 1 < mine.fs.size() ? mine.fs[f + 1] : mine.wire.len;
+        rec.ws->DeliverFrame(rec.opcode, rec.fin, base + at, size_t(end - at));
+    }
+}
+
+const uint8_t* WSReceiveBatch::Unmask(Batch& b)
+{
+    // No frame with a key to apply (unmasked frames, or key 0: the
+    // server-to-client direction of every reference session, ws.cpp:206):
+    // unmasking is the identity, exactly as the per-call path skips it, so
+    // the payloads are handed out where they lie in the batch, at the header
+    // sizes the framer recorded (b.info is not used).
+    const size_t n = b.fs.size();
+    if (!n || !b.keyed)
+        return b.wire.p;
+    if (n > UINT32_MAX)
+        throw std::length_error("WSReceiveBatch: more than 2^32-1 frames in one flush");
+    b.info.resize(n);
+    Grow(b.out, b.wire.len);
+    if (_devs.size() > 1)
+        check(wsg_decode_batch_host_multi(_devs.data(), int(_devs.size()), b.wire.p, b.wire.len, b.fs.data(),
+                                          uint32_t(n), b.out.p, b.info.data()),
+              "wsg_decode_batch_host_multi");
+    else
+        check(wsg_decode_batch_host(_devs.size() == 1 ? _devs[0] : _ctx ? _ctx : ThreadCodec(), b.wire.p, b.wire.len,
+                                    b.fs.data(), uint32_t(n), b.out.p, b.info.data()),
+              "wsg_decode_batch_host");
+    return b.out.p;
 }
 
 void WSReceiveBatch::ApplyPending(size_t from)
@@ -279,6 +384,7 @@ size_t WSReceiveBatch::Flush()
         _n_bytes.store(0, std::memory_order_relaxed);
         _flushing = true;
         _flusher = std::this_thread::get_id();
+        _pos.store(0, std::memory_order_relaxed);
     }
     Batch& b = _spare;   // this thread's until _flushing drops: Feed only touches _cur
     struct Done {
@@ -295,31 +401,7 @@ size_t WSReceiveBatch::Flush()
     } done{this};
 
     const size_t n = b.fs.size();
-    const uint8_t* payload_base = b.out.p;
-    if (n) {
-        if (n > UINT32_MAX)
-            throw std::length_error("WSReceiveBatch: more than 2^32-1 frames in one flush");
-        if (b.keyed) {
-            b.info.resize(n);
-            Grow(b.out, b.wire.len);
-            payload_base = b.out.p;
-            if (_devs.size() > 1)
-                check(wsg_decode_batch_host_multi(_devs.data(), int(_devs.size()), b.wire.p, b.wire.len, b.fs.data(),
-                                                  uint32_t(n), b.out.p, b.info.data()),
-                      "wsg_decode_batch_host_multi");
-            else
-                check(wsg_decode_batch_host(_devs.size() == 1 ? _devs[0] : _ctx ? _ctx : ThreadCodec(), b.wire.p,
-                                            b.wire.len, b.fs.data(), uint32_t(n), b.out.p, b.info.data()),
-                      "wsg_decode_batch_host");
-        }
-        // else: no frame has a key to apply (unmasked frames, or key 0: the
-        // server-to-client direction of every reference session, ws.cpp:206):
-        // unmasking is the identity, exactly as the per-call path skips it, so
-        // the payloads are handed out where they lie in the batch, at the
-        // header sizes the framer recorded (b.info is not used)
-    }
-    if (!b.keyed)
-        payload_base = b.wire.p;
+    const uint8_t* payload_base = Unmask(b);
     size_t delivered = 0;
     const void* announced = nullptr;
     // b.recs is written only by this thread (its callbacks' Forget); other
@@ -330,6 +412,7 @@ size_t WSReceiveBatch::Flush()
         // connection it already holds that connection: no store, no wake-up
         if (b.recs[r].ws != announced) {
             announced = b.recs[r].ws;
+            _pos.store(r, std::memory_order_seq_cst);   // (a Drain waits for the records from here on)
             _busy.store(announced, std::memory_order_seq_cst);
             if (_waiters.load(std::memory_order_seq_cst)) {
                 std::scoped_lock locker(_lock);   // a Forget waiting for the previous connection may go

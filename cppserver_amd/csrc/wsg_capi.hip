@@ -60,7 +60,11 @@ struct wsg_ctx {
     int fan_wpb = 1;
     uint64_t small_avg = wsg::SMALL_AVG;   // batch encode: k_encode_small when wire_cap <= n * small_avg
     unsigned long long* d_err = nullptr;        // latch of the caller-visible async entry points (wsg_sync)
-    unsigned long long* d_err_host = nullptr;   // latch of the host-staged pipelines (their own status)
+    // latches of the host-staged pipelines (their own status): [0] the
+    // decodes' (read back, re-armed after an error), [1] the encodes' (their
+    // capacity is checked on the host, so nothing they latch is read: apart,
+    // so that it never disables the decodes' latch read-back)
+    unsigned long long* d_err_host = nullptr;
     unsigned long long* h_err_copy = nullptr;   // page-locked: d_err_host after a large in-place decode
     // scratch
     wsg_enc_scratch enc;
@@ -364,9 +368,17 @@ struct LaneServer {
     uint64_t idle_ticks = 0, yield_ticks = 0, delay_ticks = 0;
     int timeout_ms = 5000;           // a request unanswered this long: the lane is given up ($WSG_LANE_TIMEOUT_MS)
     int drain_ms = 2000;             // ... and waited for this long to leave ($WSG_LANE_DRAIN_MS)
+    uint32_t delay_gens = ~0u;       // test hook: generations up to this one start late ($WSG_TEST_LANE_DELAY_GENS)
     std::mutex launch_lock;
     std::atomic<uint32_t> gen{0};        // the last launch's generation (0: none yet)
-    std::atomic<bool> broken{false};     // given up: no more launches, every caller takes the launch paths
+    std::atomic<bool> broken{false};     // given up: no launches until re-armed, every caller takes the launch paths
+    // a lane given up is re-armed (lane_rearm) once its stream has drained and
+    // this hold-off has passed: it doubles with every give-up in a row (from
+    // kRearmFirstMs up to kRearmMaxMs) and resets once a re-armed lane answers
+    std::atomic<int64_t> retry_at_ns{0};
+    uint32_t backoff_ms = 0;             // (under launch_lock)
+    std::atomic<bool> rearmed{false};    // re-armed and not yet answered a request since
+    std::atomic<uint64_t> rearms{0};
     std::atomic<uint64_t> tickets{0};    // next ticket
     std::atomic<int> inflight{0};        // requests posted and not yet answered
     std::atomic<uint64_t> launches{0};
@@ -406,6 +418,28 @@ bool lane_drained(LaneServer* s, int ms)
     }
 }
 
+// Start the lane's mailboxes at ticket `base` (a multiple of W), with no
+// launch running or queued and no request in flight: every workgroup resumes
+// at its first ticket from `base` on, and every slot counts as answered and
+// read, so the first W * LANE_RING tickets from `base` post without waiting.
+// (Slots keep their old units: every tag in them is below base + 1, and
+// every ticket from base on has a tag above that.)
+void lane_set_frontier(LaneServer* s, uint64_t base)
+{
+    const uint64_t W = s->W, R = wsg::LANE_RING;
+    for (uint32_t g = 0; g < s->W; ++g)
+        __atomic_store_n(&s->bell->next_j[g], base / W, __ATOMIC_RELAXED);
+    for (uint64_t t = base; t < base + W * R; ++t)
+        s->released[(t % W) * R + (t / W) % R].store(t >= W * R ? t - W * R + 1 : 0, std::memory_order_relaxed);
+    s->tickets.store(base);
+}
+
+int64_t steady_ns()
+{
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
 // Every lane told to leave at process exit (a lane also leaves on its own
 // after its idle limit); a lane already given up is not waited for again.
 void lanes_at_exit()
@@ -438,6 +472,8 @@ LaneServer* lane_server(int device)
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0)
         khz = 100000;   // 100 MHz, the gfx9 constant clock
     long idle_us = 2000, yield_us = 2000, delay_us = 0;
+    uint64_t ticket_base = 0;
+    bool stale_xres = false;
     {
         std::lock_guard<std::recursive_mutex> eg(wsg::env_mutex());
         if (const char* e = wsg::envp("WSG_LANE_WGS")) {
@@ -455,6 +491,12 @@ LaneServer* lane_server(int device)
             s->drain_ms = int(std::max(1l, std::min(600000l, std::atol(e))));
         if (const char* e = wsg::envp("WSG_TEST_LANE_DELAY_US"))   // test hook: the kernel starts late
             delay_us = std::max(0l, std::min(10000000l, std::atol(e)));
+        if (const char* e = wsg::envp("WSG_TEST_LANE_DELAY_GENS"))   // ... only its first launches
+            s->delay_gens = uint32_t(std::max(0l, std::min(1000000l, std::atol(e))));
+        if (const char* e = wsg::envp("WSG_TEST_LANE_TICKET_BASE"))  // test hook: the ticket counter starts here
+            ticket_base = std::strtoull(e, nullptr, 10);
+        if (const char* e = wsg::envp("WSG_TEST_LANE_STALE_XRES"))   // ... with every inline answer unit stale
+            stale_xres = *e == '1';
     }
     s->idle_ticks = uint64_t(idle_us) * uint64_t(khz) / 1000u;
     s->yield_ticks = uint64_t(yield_us) * uint64_t(khz) / 1000u;
@@ -481,19 +523,80 @@ LaneServer* lane_server(int device)
     }
     std::memset(p, 0, sizeof(wsg::LaneBell));
     s->bell = static_cast<wsg::LaneBell*>(p);
+    if (ticket_base) {
+        lane_set_frontier(s, ticket_base / s->W * s->W);
+        if (stale_xres) {
+            // every slot's inline answer units as a task 2^32 tickets before
+            // its next one would have left them: the low 32 bits of the tag
+            // are the next ticket's, the dword not its answer
+            const uint64_t b = s->tickets.load();
+            for (uint64_t t = b; t < b + uint64_t(s->W) * wsg::LANE_RING; ++t)
+                for (uint64_t& u : s->bell->xres[t % s->W][(t / s->W) % wsg::LANE_RING].u)
+                    u = (uint64_t(uint32_t(t + 1)) << 32) | 0xA5A5A5A5u;
+        }
+    }
     static std::once_flag once;
     std::call_once(once, [] { std::atexit(lanes_at_exit); });
     m[device] = s;
     return s;
 }
 
-// Give the lane up (a request went unanswered): no launch from now on, and
-// every workgroup leaves at its next check without taking another task.
+constexpr uint32_t kRearmFirstMs = 50, kRearmMaxMs = 4000;
+
+// (under launch_lock) No launch until re-armed, and every workgroup leaves at
+// its next check without taking another task; the hold-off before a re-arm
+// doubles with every give-up in a row.
+void lane_break_locked(LaneServer* s)
+{
+    if (s->broken.load())
+        return;
+    s->backoff_ms = s->backoff_ms ? std::min(kRearmMaxMs, s->backoff_ms * 2) : kRearmFirstMs;
+    s->retry_at_ns.store(steady_ns() + int64_t(s->backoff_ms) * 1000000);
+    s->rearmed.store(false);
+    s->broken.store(true);
+    __atomic_store_n(&s->bell->ctl.stop, 1u, __ATOMIC_RELEASE);
+}
+
+// Give the lane up (a request went unanswered).
 void lane_give_up(LaneServer* s)
 {
     std::lock_guard<std::mutex> g(s->launch_lock);
-    s->broken.store(true);
-    __atomic_store_n(&s->bell->ctl.stop, 1u, __ATOMIC_RELEASE);
+    lane_break_locked(s);
+}
+
+// Bring a given-up lane back: once its hold-off has passed, no request is in
+// flight (every caller of the give-up has taken its fallback and released its
+// slots) and its stream has drained (no workgroup left to write a request's
+// buffers), the mailboxes restart past every ticket handed out so far —
+// tasks posted to the old lane and never taken are skipped, not run — and
+// the next request launches a new generation.  False: still given up.
+bool lane_rearm(LaneServer* s)
+{
+    if (steady_ns() < s->retry_at_ns.load(std::memory_order_relaxed))
+        return false;
+    std::unique_lock<std::mutex> g(s->launch_lock, std::try_to_lock);
+    if (!g.owns_lock())
+        return false;
+    if (!s->broken.load())
+        return true;
+    if (s->inflight.load() != 0)
+        return false;
+    const hipError_t q = hipStreamQuery(s->stream);
+    if (q != hipSuccess) {
+        if (q != hipErrorNotReady)
+            (void)hipGetLastError();
+        s->retry_at_ns.store(steady_ns() + int64_t(s->backoff_ms) * 1000000);
+        return false;
+    }
+    const uint64_t W = s->W;
+    lane_set_frontier(s, (s->tickets.load() + W - 1) / W * W);
+    __atomic_store_n(&s->bell->ctl.stop, 0u, __ATOMIC_RELAXED);
+    // the last generation counts as ended: the next request launches
+    __atomic_store_n(&s->bell->ctl.closing, s->gen.load(), __ATOMIC_RELEASE);
+    s->rearmed.store(true);
+    s->rearms.fetch_add(1);
+    s->broken.store(false);
+    return true;
 }
 
 // Launch the next generation if generation `seen` is the last one (none yet,
@@ -507,10 +610,10 @@ void lane_relaunch(LaneServer* s, uint32_t seen)
     uint32_t next = seen + 1;
     if (next == 0)
         next = 1;
-    if (wsg::launch_lane(s->stream, s->bell, s->W, s->idle_ticks, s->yield_ticks, next, s->delay_ticks) != hipSuccess) {
+    if (wsg::launch_lane(s->stream, s->bell, s->W, s->idle_ticks, s->yield_ticks, next,
+                         next <= s->delay_gens ? s->delay_ticks : 0) != hipSuccess) {
         (void)hipGetLastError();
-        s->broken.store(true);
-        __atomic_store_n(&s->bell->ctl.stop, 1u, __ATOMIC_RELEASE);
+        lane_break_locked(s);
         return;
     }
     s->launches.fetch_add(1);
@@ -538,7 +641,9 @@ LaneServer* lane_for(wsg_ctx* c)
             return nullptr;
         }
     }
-    return c->lane->broken.load(std::memory_order_relaxed) ? nullptr : c->lane;
+    if (c->lane->broken.load(std::memory_order_relaxed) && !lane_rearm(c->lane))
+        return nullptr;
+    return c->lane;
 }
 
 // A request's frame groups: runs of whole frames [f, f + cnt), each at most
@@ -617,11 +722,15 @@ LaneResult lane_run(wsg_ctx* c, LaneServer* s, const uint64_t (*words)[wsg::LANE
 {
     *errs = 0;
     *answered = 0;
-    if (s->broken.load())
+    // in flight before the check: a re-arm (which needs none in flight while
+    // the lane is given up) never runs under a request that saw it working
+    s->inflight.fetch_add(1);
+    if (s->broken.load()) {
+        s->inflight.fetch_sub(1);
         return LANE_FALLBACK;
+    }
     const uint32_t W = s->W, R = wsg::LANE_RING;
     const uint64_t x = s->tickets.fetch_add(groups);
-    s->inflight.fetch_add(1);
     ++c->lane_requests;
     const auto t0 = std::chrono::steady_clock::now();
     auto late = [&] { return std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(s->timeout_ms); };
@@ -640,6 +749,17 @@ LaneResult lane_run(wsg_ctx* c, LaneServer* s, const uint64_t (*words)[wsg::LANE
                 __builtin_ia32_pause();
             }
         }
+#ifndef WSG_DIAG_NO_XRES_POISON   // (diagnostic build only: shows test_lane_inline_answers_across_the_tag_wrap failing)
+        if (xwords) {
+            // an inline answer's units carry only the low 32 bits of the
+            // ticket, which recur in this slot every 2^32 tickets (W * R
+            // divides 2^32), and the slot's last inline task may have been
+            // that long ago: units that tag no ticket of this lap before the
+            // task goes out (its answer has been read: `released`, above)
+            for (uint32_t q = 0; q < xwords; ++q)
+                __atomic_store_n(&s->bell->xres[wg][slot].u[q], uint64_t(~uint32_t(tk + 1)) << 32, __ATOMIC_RELAXED);
+        }
+#endif
         wsg::LaneTask* T = &s->bell->box[wg][slot];
         for (uint32_t u = wsg::LANE_WORDS; u-- > 0;) {
             T->w[u].v = words[k][u];
@@ -692,6 +812,11 @@ LaneResult lane_run(wsg_ctx* c, LaneServer* s, const uint64_t (*words)[wsg::LANE
     }
     if (!gave_up) {
         s->inflight.fetch_sub(1);
+        if (s->rearmed.load(std::memory_order_relaxed)) {   // the re-armed lane works: the next give-up's hold-off starts over
+            std::lock_guard<std::mutex> g(s->launch_lock);
+            if (s->rearmed.exchange(false) && !s->broken.load())
+                s->backoff_ms = 0;
+        }
         return LANE_DONE;
     }
     // Given up: nothing of the request may be touched until the lane has
@@ -828,14 +953,14 @@ int wsg_create(int device, wsg_ctx** out)
         if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess ||
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
             hipMalloc(&c->d_err, sizeof(unsigned long long)) != hipSuccess ||
-            hipMalloc(&c->d_err_host, sizeof(unsigned long long)) != hipSuccess ||
+            hipMalloc(&c->d_err_host, 2 * sizeof(unsigned long long)) != hipSuccess ||
             hipHostMalloc(&c->h_err_copy, sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
             wsg_destroy(c);
             return WSG_EHIP;
         }
     }
     if (hipMemsetAsync(c->d_err, 0xFF, sizeof(unsigned long long), c->stream) != hipSuccess ||
-        hipMemsetAsync(c->d_err_host, 0xFF, sizeof(unsigned long long), c->stream) != hipSuccess ||
+        hipMemsetAsync(c->d_err_host, 0xFF, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
         wsg_destroy(c);
         return WSG_EHIP;
@@ -1879,7 +2004,7 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
             }
             hipStream_t s = c->stream;
             if (int rc = encode_launch(c, s, payload, desc_dev, n, wire, wire_off[n], sl.d_woff, sl.enc,
-                                       c->d_err_host))
+                                       c->d_err_host + 1))
                 return rc;
             WSG_HIP(hipStreamSynchronize(s));
             return WSG_OK;   // capacity was checked on the host: nothing for the latch to report
@@ -1965,7 +2090,7 @@ int wsg_encode_batch_host(wsg_ctx* c, const uint8_t* payload, uint64_t payload_l
                 return rc;
             const uint64_t wlen = wire_off[g.i1] - wire_off[g.i0];
             if (int rc = encode_launch(c, pp.kern, sl.d_payload, sl.d_desc, m, sl.d_wire, wlen, sl.d_woff, sl.enc,
-                                       c->d_err_host))
+                                       c->d_err_host + 1))
                 return rc;
             if (int rc = pipe_to_d2h(pp, sl))
                 return rc;

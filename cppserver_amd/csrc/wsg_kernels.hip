@@ -75,6 +75,9 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 // (the runtime's fill of the same bytes: 97 us; profiles/r5/fan_cap_ab.log)
 #define WSG_FAN_CAP 4
 #endif
+#ifndef WSG_FAN_MANY_WPC
+#define WSG_FAN_MANY_WPC 0   // fan-out period path, many messages per launch: waves per CU per message (0: as one message)
+#endif
 #ifndef WSG_FAN_KV
 #define WSG_FAN_KV 2   // fan-out period path: key registers per lane (64 pass-window slots each)
 #endif
@@ -2267,6 +2270,8 @@ bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, int wpb, con
     if (Q * 64 > chunks * 2)   // even the fewest waves would mostly idle: leave it to the flat kernel
         return false;
     const uint64_t rows = (chunks + 63) / 64;
+    if (WSG_FAN_MANY_WPC && nmsgs > 1)
+        waves_per_cu = WSG_FAN_MANY_WPC;
     uint64_t mult = std::max<uint64_t>(1, (uint64_t(cus) * waves_per_cu + Q / 2) / Q);
     mult = std::min(mult, (rows + Q - 1) / Q);                                                 // no idle waves
     mult = std::max(mult, (chunks + Q * 64 * max_passes - 1) / (Q * 64 * max_passes));   // every pass's keys in one load per lane

@@ -180,9 +180,13 @@ public:
     void Clear(WebSocket& ws);
     //! Drop every queued frame of `ws` (call before destroying it)
     void Forget(WebSocket& ws);
-    //! Deliver every queued frame of `ws` (a connection leaving the batch):
-    //! flushes until none is queued and no other thread's flush is running.
-    //! From inside a callback of this thread's own flush it returns at once.
+    //! Deliver every queued frame of `ws` (a connection leaving the batch),
+    //! in order, on the calling thread.  It waits only while another
+    //! thread's flush still has frames of ws to deliver (never for the rest
+    //! of that flush); ws's frames still queued then are unmasked and
+    //! delivered here without the others, and with no flush running the
+    //! whole queue is flushed.  From inside a callback of this thread's own
+    //! flush it returns at once.
     void Drain(WebSocket& ws);
     //! Unmask every queued frame on the GPU and deliver them in arrival
     //! order; returns the number of frames delivered.  A Flush() called from
@@ -228,6 +232,10 @@ private:
 
     void Emit(WebSocket& ws, const uint8_t* frame, uint64_t total, uint32_t hdr, const uint8_t* key);
     void ApplyPending(size_t from);
+    //! the batch's GPU pass (when a frame has a key); where the payloads lie
+    const uint8_t* Unmask(Batch& b);
+    //! this thread's Drain delivery in progress (its records), or nullptr
+    static std::vector<Rec>*& DrainRecs();
     static void Grow(Pinned& b, uint64_t need);
     static void Release(Pinned& b);
 
@@ -239,7 +247,8 @@ private:
     std::vector<WebSocket*> _pending;    // other threads' Forget()s the flush has not applied yet
     std::atomic<bool> _has_pending{false};
     std::atomic<const void*> _busy{nullptr};   // the connection the flush is at (announced before its Forget check)
-    std::atomic<int> _waiters{0};              // Forget()s waiting for _busy to move on
+    std::atomic<size_t> _pos{0};               // the first record of that connection's run (a Drain waits past ws's)
+    std::atomic<int> _waiters{0};              // Forget()s / Drain()s waiting for _busy / _pos to move on
     std::condition_variable_any _busy_cv;
     std::atomic<size_t> _n_frames{0};          // _cur.fs.size(), written under _lock
     std::atomic<uint64_t> _n_bytes{0};         // _cur.wire.len, written under _lock

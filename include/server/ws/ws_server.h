@@ -12,6 +12,7 @@
 #include "server/ws/ws_session.h"
 
 #include <memory>
+#include <mutex>
 #include <shared_mutex>
 #include <vector>
 
@@ -80,6 +81,10 @@ private:
     std::shared_ptr<WSReceiveBatch> _rx_batch;
     std::shared_ptr<WSSendBatch> _tx_batch;
     std::vector<int> _batch_devices;
+    // one EnableBatchReceive at a time: its sessions switch batches outside
+    // the sessions lock (a switch delivers their queued frames, whose
+    // callbacks may take that lock)
+    std::recursive_mutex _rx_switch;
 
     mutable std::shared_mutex _sessions_lock;
     std::vector<std::shared_ptr<WSSession>> _sessions;

@@ -349,15 +349,19 @@ int wsg_timing_minmax(wsg_ctx* ctx, double* min_ms, double* max_ms);
  * without a task and after $WSG_LANE_YIELD_US (default 2000) of running (a
  * running kernel holds up calls that wait for the device to drain); the next
  * call launches it again.  A request unanswered for $WSG_LANE_TIMEOUT_MS
- * (default 5000) gives the lane up for the process: the caller waits up to
+ * (default 5000) gives the lane up: the caller waits up to
  * $WSG_LANE_DRAIN_MS (default 2000) for it to leave and then takes the
  * launch path, or, if it does not leave, returns WSG_EHIP without touching
  * the buffers (the lane may still write them) and the context returns
- * WSG_EHIP from then on.  The lane's settings are read when a process first
- * uses a device's lane.
+ * WSG_EHIP from then on (a device free in another context, e.g. its
+ * wsg_destroy, waits for that lane to leave).  A lane given up comes back on
+ * a later call once it has left, no request is in flight and a hold-off has
+ * passed (50 ms, doubling with each give-up in a row up to 4 s); tasks the
+ * old lane never took are skipped, not run.  The lane's settings are read
+ * when a process first uses a device's lane.
  * Requests this context put on the lane, the launches of the device's lane,
- * and whether it runs now (1), has left (0) or was given up (-1: the launch
- * paths from then on).                                                      */
+ * and whether it runs now (1), has left (0) or is given up (-1: the launch
+ * paths until it comes back).                                               */
 int wsg_lane_stats(wsg_ctx* ctx, uint64_t* requests, uint64_t* launches, int* running);
 
 #ifdef __cplusplus

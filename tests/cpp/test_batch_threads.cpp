@@ -350,6 +350,73 @@ protected:
     }
 };
 
+// Two threads flushing at once, each from inside a callback moving a session
+// off the batch the OTHER thread is flushing (SetReceiveBatch -> Drain), with
+// the session's frames queued there after that flush began (Drain
+// waited for the other thread's whole flush, so each waited for the other).
+// Drain now waits only for the session's own frames in the running flush and
+// delivers those still queued itself.  The moved session gets its frame
+// exactly once, before SetReceiveBatch returns.  A watchdog ends the process
+// if the flushes block on each other.
+static void test_cross_thread_drain_in_callbacks()
+{
+    for (int iter = 0; iter < 50; ++iter) {
+        struct State {
+            WSReceiveBatch x{nullptr}, y{nullptr};
+            Trigger tx, ty;
+            Sink sink_x, sink_y;
+            CountSession sx{sink_x}, sy{sink_y};   // attached to y / x, moved off them by thread A / B
+            std::mutex m;
+            std::condition_variable cv;
+            int inside = 0;
+            std::atomic<int> done{0};
+        };
+        auto st = std::make_unique<State>();
+        State& S = *st;
+        S.sx.Ready();
+        S.sy.Ready();
+        S.sx.SetReceiveBatch(&S.y);
+        S.sy.SetReceiveBatch(&S.x);
+        const std::vector<uint8_t> f = unmasked_frame(24, 0x33);
+        auto both_inside = [&] {
+            std::unique_lock<std::mutex> g(S.m);
+            ++S.inside;
+            S.cv.notify_all();
+            S.cv.wait(g, [&] { return S.inside == 2; });
+        };
+        auto move_off = [&](CountSession& s) {
+            s.onReceived(f.data(), f.size());   // queued in the batch the other thread is flushing
+            s.SetReceiveBatch(nullptr);         // delivered before this returns
+            CHECK(s.bytes.load() == 24);
+        };
+        S.tx.on_first = [&] { both_inside(); move_off(S.sx); };
+        S.ty.on_first = [&] { both_inside(); move_off(S.sy); };
+        auto run = [&](WSReceiveBatch& mine, Trigger& t) {
+            mine.Feed(t, f.data(), f.size());
+            mine.Flush();
+            ++S.done;
+        };
+        std::thread watchdog([&] {
+            for (int i = 0; i < 200 && S.done.load() < 2; ++i)
+                std::this_thread::sleep_for(std::chrono::milliseconds(100));
+            if (S.done.load() < 2) {
+                std::fprintf(stderr, "cross-thread drain: flushes blocked on each other\n");
+                std::_Exit(3);
+            }
+        });
+        std::thread a([&] { run(S.x, S.tx); });
+        std::thread b([&] { run(S.y, S.ty); });
+        a.join();
+        b.join();
+        watchdog.join();
+        CHECK(S.tx.calls.load() == 1 && S.ty.calls.load() == 1);
+        // nothing of theirs left behind to deliver twice
+        S.x.Flush();
+        S.y.Flush();
+        CHECK(S.sx.bytes.load() == 24 && S.sy.bytes.load() == 24);
+    }
+}
+
 // IO threads feed their sessions' reads (RouteFrames) and send synchronously
 // (SendFrame flushes the send batch) while another thread switches the
 // server's batched receive and send on and off and a third flushes: no read
@@ -424,6 +491,7 @@ int main()
         test_cross_thread_destroy_in_callbacks(false);
     if (!std::getenv("ONLY_EXPLICIT"))
         test_cross_thread_destroy_in_callbacks(true);
+    test_cross_thread_drain_in_callbacks();
     std::printf("%d checks, %d failures\n", g_checks.load(), g_failures.load());
     return g_failures.load() == 0 ? 0 : 1;
 }

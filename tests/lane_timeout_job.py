@@ -1,12 +1,14 @@
-"""One case of test_gpu_lane.py::test_lane_timeout_waits_for_the_lane, in a
-process of its own (the lane given up is the process's, for good).  The
-environment holds the lane back ($WSG_TEST_LANE_DELAY_US) longer than a
-request may wait ($WSG_LANE_TIMEOUT_MS):
+"""One case of test_gpu_lane.py::test_lane_timeout_waits_for_the_lane (or
+test_lane_inline_answers_across_the_tag_wrap), in a process of its own (the
+lane is the process's).  The environment holds the lane's first launch back
+($WSG_TEST_LANE_DELAY_US, $WSG_TEST_LANE_DELAY_GENS) longer than a request
+may wait ($WSG_LANE_TIMEOUT_MS):
 
 * drained: the lane leaves within $WSG_LANE_DRAIN_MS, so the call decodes on
   the launch path and returns the oracle's bytes; nothing is written into the
   buffers after it returned (the late lane saw `stop` and did not take the
-  request); the next batch in the same buffers (launch path) is exact too;
+  request); then the lane comes back: the next batch in the same buffers and
+  200 per-call XORs are lane requests of a new launch, all exact;
 * lost: the lane does not leave in time: the call fails (WSG_EHIP) without
   the buffers being touched — not by the launch path, and not by the late
   lane once it runs — and the context refuses further calls.
@@ -15,6 +17,8 @@ request may wait ($WSG_LANE_TIMEOUT_MS):
   $WSG_LANE_IDLE_US of tens of microseconds) while eight threads, each with
   its own context, decode, encode and XOR through it: every result exact,
   hundreds of launches, no request lost across a hand-over.
+
+* wrap: see wrap() below.
 
 Prints one JSON line {"ok": bool, ...}."""
 import json
@@ -40,6 +44,37 @@ def batch(seed):
     payload = wl.random_bytes(rng, total + 16)
     wire, off = oracle.encode_batch(payload, desc)
     return wire, off[:-1].copy()
+
+
+def xor_ref(data, key, phase):
+    """ws.cpp:264-270 (and :402-403): byte i ^ key byte (phase + i) % 4."""
+    kb = np.frombuffer(int(key).to_bytes(4, "little"), np.uint8)
+    return np.frombuffer(bytes(data), np.uint8) ^ kb[(np.arange(len(data)) + phase) % 4]
+
+
+def wrap(res):
+    """Tickets from just below 2^32 ($WSG_TEST_LANE_TICKET_BASE) with every
+    slot's inline answer units left as a task 2^32 tickets earlier would have
+    left them ($WSG_TEST_LANE_STALE_XRES): per-call XORs of up to 40 bytes
+    (answered inline) and larger ones, across the 2^32 mark and round the
+    ring more than once — every result the request's own bytes."""
+    c = ca.Codec(0)
+    rng = np.random.default_rng(11)
+    req0 = c.lane_stats()[0]
+    bad = []
+    n = 3000
+    for i in range(n):
+        ln = int(rng.integers(1, 41)) if i % 5 else int(rng.integers(41, 300))
+        data = bytes(wl.random_bytes(rng, ln))
+        key, phase = int(rng.integers(0, 2**32)), int(rng.integers(0, 4))
+        got = np.frombuffer(c.xor_host(data, key, phase), np.uint8)
+        if not np.array_equal(got, xor_ref(data, key, phase)):
+            bad.append((i, ln))
+    req1, launches, running = c.lane_stats()
+    res.update(bad=bad[:10], n_bad=len(bad), requests=req1 - req0, launches=launches, running=running)
+    res["ok"] = bool(not bad and req1 - req0 == n and running != -1)
+    c.close()
+    print(json.dumps(res))
 
 
 def handover(res):
@@ -104,6 +139,8 @@ def main():
     case = sys.argv[1]
     if case == "handover":
         return handover({"case": case})
+    if case == "wrap":
+        return wrap({"case": case})
     res = {"case": case}
     c = ca.Codec(0)
     wire, fs = batch(1)
@@ -121,13 +158,28 @@ def main():
         snap = np.array(pin_out)
         time.sleep(1.0)   # the late lane has long run by now
         untouched_after = np.array_equal(np.array(pin_out), snap)
+        req0, launches0, _ = c.lane_stats()
+        # the lane comes back (hold-off passed, it has left, nothing in
+        # flight; only its first launch was held back): the next batches and
+        # per-call XORs are lane requests of a new launch, exact
         wire2, fs2 = batch(2)
         rc2_o, out2_o, _ = oracle.decode_batch(wire2, fs2)
         pin_in[: len(wire2)] = wire2
         rc2, out2, _ = c.decode_batch_host(pin_in[: len(wire2)], fs2, out=pin_out)
         second = rc2 == rc2_o and np.array_equal(out2, out2_o)
-        res.update(first=first, untouched_after=untouched_after, second=second)
-        res["ok"] = bool(first and untouched_after and second and res["running"] == -1)
+        rng = np.random.default_rng(3)
+        xor_ok = True
+        for i in range(200):
+            data = bytes(wl.random_bytes(rng, int(rng.integers(1, 200))))
+            key, phase = int(rng.integers(0, 2**32)), i % 4
+            xor_ok &= bool(np.array_equal(np.frombuffer(c.xor_host(data, key, phase), np.uint8),
+                                          xor_ref(data, key, phase)))
+        req1, launches1, running1 = c.lane_stats()
+        back = req1 - req0 >= 201 and launches1 > launches0 and running1 != -1
+        res.update(first=first, untouched_after=untouched_after, second=second, xor_ok=xor_ok,
+                   lane_back=bool(back), requests=[req0, req1], launches=[launches0, launches1],
+                   running_after=running1)
+        res["ok"] = bool(first and untouched_after and second and xor_ok and back and res["running"] == -1)
     else:
         time.sleep(1.5)   # the late lane starts (0.9 s) and must leave without the request
         untouched = bool(np.all(np.array(pin_out) == 0xEE))

@@ -410,8 +410,8 @@ def test_bench_n2_c5_rank_form():
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, WSG_BENCH_SHARE_DEVICES="1", WSG_C5_FRAMES="16384", WSG_BENCH_TORCH_GATHER="0",
-               WSG_BENCH_CAPI_RCCL="0", WSG_BENCH_HOST_LEGS="0")
+    env = dict(os.environ, WSG_BENCH_SHARE_DEVICES="1", WSG_C5_FRAMES="16384", WSG_BENCH_CAPI_RCCL="0",
+               WSG_BENCH_HOST_LEGS="0", NCCL_DEBUG="VERSION")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(root, "bench.py"),
                         "--gpus", "2", "--steps", "5", "--warmup", "2", "--no-extras"],
@@ -424,3 +424,10 @@ def test_bench_n2_c5_rank_form():
     assert c5["path"].startswith("C-ABI rank form")
     assert c5["roofline_per_rank"]["kernel"] == "k_encode_mask" and c5["roofline_per_rank"]["frac"] > 0
     assert c5["bytes_into_root"] == 16384 // 2 * (16384 + 8)
+    # one RCCL stack per rank: the bench's own group is gloo, so the only RCCL
+    # initialised is the one the product library loads (torch's bundled RCCL,
+    # another version, would print its own banner)
+    import re
+
+    versions = set(re.findall(r"RCCL version\s*:\s*(\S+)", r.stdout + r.stderr))
+    assert len(versions) == 1, versions

@@ -514,29 +514,45 @@ def test_lane_per_call_xor(lane, launch):
     assert r1 - r0 == 4 * sum(1 for ln in lens if ln <= 65536), (r0, r1)
 
 
-def test_lane_timeout_waits_for_the_lane():
-    """A request the lane leaves unanswered ($WSG_LANE_TIMEOUT_MS; the lane
-    held back by $WSG_TEST_LANE_DELAY_US) in a process of its own: the caller
-    gives the lane up and waits for it to leave before the launch path reuses
-    the buffers; the late lane does not take the abandoned request (nothing
-    written after the call returned); and when the lane does not leave in
-    time, the call fails without touching the buffers and the context refuses
-    further calls.  And the lane handing over every few tens of
-    microseconds while eight threads' contexts use it: every result exact,
-    no request lost across a hand-over."""
+def _lane_job(case, env):
     import json
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     job = os.path.join(root, "tests", "lane_timeout_job.py")
+    e = dict(os.environ, **env)
+    r = subprocess.run([sys.executable, job, case], env=e, capture_output=True, text=True, timeout=90, cwd=root)
+    assert r.returncode == 0, (case, r.stdout[-2000:], r.stderr[-2000:])
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["ok"], (case, res)
+
+
+def test_lane_inline_answers_across_the_tag_wrap():
+    """An inline XOR's answer units carry the low 32 bits of its ticket, which
+    recur in a slot every 2^32 tickets: the host marks the slot's units stale
+    before each task goes out.  In a process of its own, tickets start just
+    below 2^32 with every slot's units left as the task 2^32 tickets earlier
+    would have left them; 3000 per-call XORs cross the mark and the ring
+    several times, every one on the lane and equal to ws.cpp:264-270's
+    bytes."""
+    _lane_job("wrap", {"WSG_TEST_LANE_TICKET_BASE": str(2**32 - 300), "WSG_TEST_LANE_STALE_XRES": "1"})
+
+
+def test_lane_timeout_waits_for_the_lane():
+    """A request the lane leaves unanswered ($WSG_LANE_TIMEOUT_MS; the lane
+    held back by $WSG_TEST_LANE_DELAY_US) in a process of its own: the caller
+    gives the lane up and waits for it to leave before the launch path reuses
+    the buffers; the late lane does not take the abandoned request (nothing
+    written after the call returned), and the lane comes back for the next
+    calls (a new launch, every result exact); and when the lane does not leave in
+    time, the call fails without touching the buffers and the context refuses
+    further calls.  And the lane handing over every few tens of
+    microseconds while eight threads' contexts use it: every result exact,
+    no request lost across a hand-over."""
     for case, env in (("drained", {"WSG_LANE_TIMEOUT_MS": "150", "WSG_TEST_LANE_DELAY_US": "500000",
-                                   "WSG_LANE_DRAIN_MS": "3000"}),
+                                   "WSG_TEST_LANE_DELAY_GENS": "1", "WSG_LANE_DRAIN_MS": "3000"}),
                       ("lost", {"WSG_LANE_TIMEOUT_MS": "100", "WSG_TEST_LANE_DELAY_US": "900000",
                                 "WSG_LANE_DRAIN_MS": "100"}),
                       ("handover", {"WSG_LANE_YIELD_US": "40", "WSG_LANE_IDLE_US": "20"})):
-        e = dict(os.environ, **env)
-        r = subprocess.run([sys.executable, job, case], env=e, capture_output=True, text=True, timeout=90, cwd=root)
-        assert r.returncode == 0, (case, r.stdout[-2000:], r.stderr[-2000:])
-        res = json.loads(r.stdout.strip().splitlines()[-1])
-        assert res["ok"], (case, res)
+        _lane_job(case, env)
