@@ -561,6 +561,14 @@ void lane_break_locked(LaneServer* s)
 void lane_give_up(LaneServer* s)
 {
     std::lock_guard<std::mutex> g(s->launch_lock);
+#ifdef WSG_DIAG_LANE   // (diagnostic build: where the mailboxes stand at a give-up)
+    std::fprintf(stderr, "lane give-up: tickets %llu gen %u closing %u stop %u\n",
+                 (unsigned long long)s->tickets.load(), s->gen.load(), s->bell->ctl.closing, s->bell->ctl.stop);
+    for (uint32_t q = 0; q < s->W; ++q)
+        std::fprintf(stderr, "  wg %u next_j %llu slot %llu tag0 %llu\n", q, (unsigned long long)s->bell->next_j[q],
+                     (unsigned long long)(s->bell->next_j[q] % wsg::LANE_RING),
+                     (unsigned long long)s->bell->box[q][s->bell->next_j[q] % wsg::LANE_RING].w[0].tag);
+#endif
     lane_break_locked(s);
 }
 

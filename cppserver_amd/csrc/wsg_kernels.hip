@@ -299,10 +299,12 @@ namespace {
 
 // A wave-uniform value computed by vector instructions, moved to SGPRs.
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+// (the builtins return int: each half goes through uint32_t, else a low half
+// of 2^31 or more sign-extends over the high one)
 __device__ __forceinline__ uint64_t uni(uint64_t x)
 {
-    return uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(x))) |
-           (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(x >> 32))) << 32);
+    return uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(x)))) |
+           (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(x >> 32)))) << 32);
 }
 
 // Frame [s, limit) as PrepareReceiveFrame parses it when delivered whole
@@ -1722,8 +1724,11 @@ __global__ __launch_bounds__(LANE_THREADS) void k_lane(LaneBell* __restrict__ be
                     why = 3;   // another workgroup of this launch left: follow
                     break;
                 }
-                const uint64_t tag0 = uint64_t(__builtin_amdgcn_readlane(u.z, 0)) |
-                                      (uint64_t(__builtin_amdgcn_readlane(u.w, 0)) << 32);
+                // (through uint32_t: readlane returns int, and a tag whose low
+                // word is 2^31 or more must not sign-extend — every ticket from
+                // 2^31 - 1 on would never be taken)
+                const uint64_t tag0 = uint64_t(uint32_t(__builtin_amdgcn_readlane(u.z, 0))) |
+                                      (uint64_t(uint32_t(__builtin_amdgcn_readlane(u.w, 0))) << 32);
                 if (tag0 == want) {
                     if (__ballot(t < LANE_WORDS && tag != want) == 0) {
                         go = 1;
@@ -1909,7 +1914,7 @@ __global__ __launch_bounds__(BLOCK) void k_fanout_flat(const uint8_t* __restrict
         uint64_t i0 = 0, r0 = 0;
         if (big) {
             // frame of the pass row's first chunk: one scalar division per row
-            i0 = __builtin_amdgcn_readfirstlane(uint32_t((base * CHUNK) / fsize));
+            i0 = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t((base * CHUNK) / fsize)));
             r0 = base * CHUNK - i0 * fsize;
         }
 #pragma unroll
