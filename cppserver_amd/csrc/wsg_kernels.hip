@@ -68,15 +68,24 @@ constexpr int MAXF = 4;   // frames a tile may touch and still take the boundary
 #ifndef WSG_FAN_UNROLL
 #define WSG_FAN_UNROLL 1   // fan-out period path: passes per loop iteration (A/B)
 #endif
+// Fan-out period path, many messages per launch (wsg_fanout_encode_many, the
+// ws_multicast tick).  Round 5 capped the launch at 4 resident one-wave
+// workgroups per CU (a dynamic LDS reserve the kernel does not use) with the
+// single message's ~6 waves per CU per message: 16 x C4 in 111-113 us, 0.86-0.88
+// of the runtime's fill of the same bytes (97 us).  Uncapped (register-limited
+// residency) with ~46 waves per CU per message — 23 x Q = 11799 waves for
+// C4, each 3-4 passes — it is 100.7-104 us, 0.93-0.97 of the fill; fewer or more
+// waves lose it on both sides (24: 121 us, 36: 117, 56: 113, 64: 124, 96: 169,
+// where one-wave workgroups come faster than the dispatcher launches them),
+// and so does the cap at these counts (profiles/r6/fan_*_ab*.log).
 #ifndef WSG_FAN_CAP
-// fan-out period path, many messages per launch: at most this many (one-wave)
-// workgroups per CU, by a dynamic LDS reserve the kernel does not use; the
-// register-limited 7 per SIMD wrote 16 x C4 in 121 us, 4 per CU in 112-114
-// (the runtime's fill of the same bytes: 97 us; profiles/r5/fan_cap_ab.log)
-#define WSG_FAN_CAP 4
+#define WSG_FAN_CAP 0   // workgroups per CU of a many-message launch (0: no cap)
 #endif
 #ifndef WSG_FAN_MANY_WPC
-#define WSG_FAN_MANY_WPC 0   // fan-out period path, many messages per launch: waves per CU per message (0: as one message)
+#define WSG_FAN_MANY_WPC 46   // waves per CU per message of a many-message launch (0: as one message)
+#endif
+#ifndef WSG_FAN_MANY_WPB
+#define WSG_FAN_MANY_WPB 0   // ... and waves per workgroup (0: as one message)
 #endif
 #ifndef WSG_FAN_KV
 #define WSG_FAN_KV 2   // fan-out period path: key registers per lane (64 pass-window slots each)
@@ -2277,6 +2286,8 @@ bool launch_fanout_period(hipStream_t s, int cus, int waves_per_cu, int wpb, con
     const uint64_t rows = (chunks + 63) / 64;
     if (WSG_FAN_MANY_WPC && nmsgs > 1)
         waves_per_cu = WSG_FAN_MANY_WPC;
+    if (WSG_FAN_MANY_WPB && nmsgs > 1)
+        wpb = WSG_FAN_MANY_WPB;
     uint64_t mult = std::max<uint64_t>(1, (uint64_t(cus) * waves_per_cu + Q / 2) / Q);
     mult = std::min(mult, (rows + Q - 1) / Q);                                                 // no idle waves
     mult = std::max(mult, (chunks + Q * 64 * max_passes - 1) / (Q * 64 * max_passes));   // every pass's keys in one load per lane
