@@ -110,6 +110,7 @@ def lib(path=None):
         "wsg_timing_read": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ci]),
         "wsg_timing_minmax": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
         "wsg_lane_stats": (ci, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(ci)]),
+        "wsg_lane_events": (ci, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         if path is not None and not hasattr(L, name):
@@ -378,6 +379,12 @@ class Codec:
         _check(self._L.wsg_lane_stats(self._ctx, ctypes.byref(r), ctypes.byref(l), ctypes.byref(on)),
                "wsg_lane_stats")
         return r.value, l.value, on.value
+
+    def lane_events(self):
+        """(give-ups, re-arms) of the device's lane — wsg_lane_events."""
+        g, r = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self._L.wsg_lane_events(self._ctx, ctypes.byref(g), ctypes.byref(r)), "wsg_lane_events")
+        return g.value, r.value
 
     def timing_read(self, reset=True):
         ms, n = ctypes.c_double(), ctypes.c_uint64()

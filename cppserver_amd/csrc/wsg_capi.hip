@@ -378,7 +378,8 @@ struct LaneServer {
     std::atomic<int64_t> retry_at_ns{0};
     uint32_t backoff_ms = 0;             // (under launch_lock)
     std::atomic<bool> rearmed{false};    // re-armed and not yet answered a request since
-    std::atomic<uint64_t> rearms{0};
+    std::atomic<uint64_t> give_ups{0}, rearms{0};   // (wsg_lane_events)
+    uint32_t delay_every = 0;            // test hook: every launch whose generation it divides starts late too ($WSG_TEST_LANE_DELAY_EVERY)
     std::atomic<uint64_t> tickets{0};    // next ticket
     std::atomic<int> inflight{0};        // requests posted and not yet answered
     std::atomic<uint64_t> launches{0};
@@ -493,6 +494,11 @@ LaneServer* lane_server(int device)
             delay_us = std::max(0l, std::min(10000000l, std::atol(e)));
         if (const char* e = wsg::envp("WSG_TEST_LANE_DELAY_GENS"))   // ... only its first launches
             s->delay_gens = uint32_t(std::max(0l, std::min(1000000l, std::atol(e))));
+        if (const char* e = wsg::envp("WSG_TEST_LANE_DELAY_EVERY")) {   // ... or every n-th (then only those
+            s->delay_every = uint32_t(std::max(0l, std::min(1000000l, std::atol(e))));   //  and the first GENS)
+            if (!wsg::envp("WSG_TEST_LANE_DELAY_GENS"))
+                s->delay_gens = 0;
+        }
         if (const char* e = wsg::envp("WSG_TEST_LANE_TICKET_BASE"))  // test hook: the ticket counter starts here
             ticket_base = std::strtoull(e, nullptr, 10);
         if (const char* e = wsg::envp("WSG_TEST_LANE_STALE_XRES"))   // ... with every inline answer unit stale
@@ -553,6 +559,7 @@ void lane_break_locked(LaneServer* s)
     s->backoff_ms = s->backoff_ms ? std::min(kRearmMaxMs, s->backoff_ms * 2) : kRearmFirstMs;
     s->retry_at_ns.store(steady_ns() + int64_t(s->backoff_ms) * 1000000);
     s->rearmed.store(false);
+    s->give_ups.fetch_add(1);
     s->broken.store(true);
     __atomic_store_n(&s->bell->ctl.stop, 1u, __ATOMIC_RELEASE);
 }
@@ -619,7 +626,8 @@ void lane_relaunch(LaneServer* s, uint32_t seen)
     if (next == 0)
         next = 1;
     if (wsg::launch_lane(s->stream, s->bell, s->W, s->idle_ticks, s->yield_ticks, next,
-                         next <= s->delay_gens ? s->delay_ticks : 0) != hipSuccess) {
+                         next <= s->delay_gens || (s->delay_every && next % s->delay_every == 0) ? s->delay_ticks
+                                                                                                 : 0) != hipSuccess) {
         (void)hipGetLastError();
         lane_break_locked(s);
         return;
@@ -2195,6 +2203,18 @@ int wsg_lane_stats(wsg_ctx* c, uint64_t* requests, uint64_t* launches, int* runn
         const uint32_t g = s ? s->gen.load() : 0;
         *running = !s ? 0 : s->broken.load() ? -1 : (g && __atomic_load_n(&s->bell->ctl.closing, __ATOMIC_ACQUIRE) != g) ? 1 : 0;
     }
+    return WSG_OK;
+}
+
+int wsg_lane_events(wsg_ctx* c, uint64_t* give_ups, uint64_t* rearms)
+{
+    if (!c)
+        return WSG_EINVAL;
+    LaneServer* s = c->lane;
+    if (give_ups)
+        *give_ups = s ? s->give_ups.load() : 0;
+    if (rearms)
+        *rearms = s ? s->rearms.load() : 0;
     return WSG_OK;
 }
 

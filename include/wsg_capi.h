@@ -363,6 +363,10 @@ int wsg_timing_minmax(wsg_ctx* ctx, double* min_ms, double* max_ms);
  * and whether it runs now (1), has left (0) or is given up (-1: the launch
  * paths until it comes back).                                               */
 int wsg_lane_stats(wsg_ctx* ctx, uint64_t* requests, uint64_t* launches, int* running);
+/* How often the device's lane was given up (a request unanswered for
+ * $WSG_LANE_TIMEOUT_MS, or a launch that failed) and brought back since the
+ * process first used it.                                                    */
+int wsg_lane_events(wsg_ctx* ctx, uint64_t* give_ups, uint64_t* rearms);
 
 #ifdef __cplusplus
 }

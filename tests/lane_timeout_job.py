@@ -18,6 +18,12 @@ may wait ($WSG_LANE_TIMEOUT_MS):
   its own context, decode, encode and XOR through it: every result exact,
   hundreds of launches, no request lost across a hand-over.
 
+* churn: the same eight threads while every few launches of the lane start
+  late ($WSG_TEST_LANE_DELAY_EVERY) past the request time-out: the lane is
+  given up and brought back again and again (wsg_lane_events), requests in
+  flight at each give-up are redone on the launch paths, tasks the old lane
+  never took are skipped; every result exact, and the lane answers after.
+
 * wrap: see wrap() below.
 
 Prints one JSON line {"ok": bool, ...}."""
@@ -77,7 +83,7 @@ def wrap(res):
     print(json.dumps(res))
 
 
-def handover(res):
+def handover(res, churn=False):
     import threading
 
     import oracle as orc
@@ -130,6 +136,18 @@ def handover(res):
     res.update(errors=errors[:5], alive=sum(th.is_alive() for th in threads), launches=stats[0][1],
                requests=sum(s[0] for s in stats), running=stats[0][2])
     res["ok"] = bool(not errors and res["alive"] == 0 and res["launches"] >= 50 and res["running"] != -1)
+    if churn:
+        # given up and brought back again and again under the eight threads,
+        # every result still exact; and the lane serves requests afterwards
+        r0 = codecs[0].lane_stats()[0]
+        time.sleep(0.3)   # past the last hold-off
+        data = bytes(range(40))
+        back = bool(np.array_equal(np.frombuffer(codecs[0].xor_host(data, 0x01020304, 1), np.uint8),
+                                   xor_ref(data, 0x01020304, 1)))
+        back &= codecs[0].lane_stats()[0] > r0 and codecs[0].lane_stats()[2] != -1
+        give_ups, rearms = codecs[0].lane_events()
+        res.update(give_ups=give_ups, rearms=rearms, lane_back=back)
+        res["ok"] = bool(not errors and res["alive"] == 0 and give_ups >= 2 and rearms >= 2 and back)
     for c in codecs:
         c.close()
     print(json.dumps(res))
@@ -139,6 +157,8 @@ def main():
     case = sys.argv[1]
     if case == "handover":
         return handover({"case": case})
+    if case == "churn":
+        return handover({"case": case}, churn=True)
     if case == "wrap":
         return wrap({"case": case})
     res = {"case": case}

@@ -525,7 +525,7 @@ def _lane_job(case, env):
     r = subprocess.run([sys.executable, job, case], env=e, capture_output=True, text=True, timeout=90, cwd=root)
     assert r.returncode == 0, (case, r.stdout[-2000:], r.stderr[-2000:])
     res = json.loads(r.stdout.strip().splitlines()[-1])
-    assert res["ok"], (case, res)
+    assert res["ok"], (case, json.dumps(res))
 
 
 def test_lane_inline_answers_across_the_tag_wrap():
@@ -549,10 +549,14 @@ def test_lane_timeout_waits_for_the_lane():
     time, the call fails without touching the buffers and the context refuses
     further calls.  And the lane handing over every few tens of
     microseconds while eight threads' contexts use it: every result exact,
-    no request lost across a hand-over."""
+    no request lost across a hand-over; and the same while the lane is given
+    up and brought back again and again (churn)."""
     for case, env in (("drained", {"WSG_LANE_TIMEOUT_MS": "150", "WSG_TEST_LANE_DELAY_US": "500000",
                                    "WSG_TEST_LANE_DELAY_GENS": "1", "WSG_LANE_DRAIN_MS": "3000"}),
                       ("lost", {"WSG_LANE_TIMEOUT_MS": "100", "WSG_TEST_LANE_DELAY_US": "900000",
                                 "WSG_LANE_DRAIN_MS": "100"}),
-                      ("handover", {"WSG_LANE_YIELD_US": "40", "WSG_LANE_IDLE_US": "20"})):
+                      ("handover", {"WSG_LANE_YIELD_US": "40", "WSG_LANE_IDLE_US": "20"}),
+                      ("churn", {"WSG_LANE_YIELD_US": "400", "WSG_LANE_IDLE_US": "200", "WSG_LANE_TIMEOUT_MS": "30",
+                                 "WSG_TEST_LANE_DELAY_US": "60000", "WSG_TEST_LANE_DELAY_EVERY": "4",
+                                 "WSG_LANE_DRAIN_MS": "3000"})):
         _lane_job(case, env)

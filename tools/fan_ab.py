@@ -11,7 +11,7 @@ Used for profiles/r5/fan_run_ab.log (a run kernel, since removed: each wave
 writing U consecutive rows with per-chunk L2 loads, 17-22 us per C4), and
 fan_cap_ab.log (the period kernel's workgroups per CU capped).
 
-usage: python tools/fan_ab.py NAME=path/to/libwsg.so ...   ($K, $ROUNDS)
+usage: python tools/fan_ab.py NAME=path/to/libwsg.so ...   ($K, $ROUNDS, $M: messages per tick, 16)
 (one variant per process: each library's initial-exec TLS)"""
 import json
 import os
@@ -60,7 +60,7 @@ def main():
     fsz = ca.frame_size(0x82, True, len(payload))
     p = torch.from_numpy(payload).cuda()
     kt = torch.from_numpy(keys.view(np.int32)).cuda()
-    m = 16
+    m = int(os.environ.get("M", 16))
     arena = torch.from_numpy(np.random.default_rng(99).integers(0, 256, m * 4096, dtype=np.uint8)).cuda()
     src = np.arange(m, dtype=np.uint64) * np.uint64(4096)
     lens = np.full(m, 4096, dtype=np.uint64)
@@ -115,7 +115,7 @@ def main():
         c4 = statistics.median(v["c4"])
         tick = statistics.median(v["tick"])
         fill = statistics.median(v["fill"])
-        print(json.dumps({"variant": v["name"], "parity_bad": v["bad"][:5], "c4_ok": v["c4_ok"],
+        print(json.dumps({"variant": v["name"], "m": m, "parity_bad": v["bad"][:5], "c4_ok": v["c4_ok"],
                           "c4_us": round(c4, 3), "c4_frac": round(41040000 / (c4 * 1e-6) / 8e12, 4),
                           "tick_us": round(tick, 2), "fill_us": round(fill, 2), "tick_vs_fill": round(fill / tick, 4),
                           "c4_all": [round(x, 3) for x in v["c4"]], "tick_all": [round(x, 1) for x in v["tick"]]}),
