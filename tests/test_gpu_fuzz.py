@@ -139,3 +139,42 @@ def test_fuzz_fanout_vs_oracle(codec, seed):
     bad = np.nonzero(got[: len(ref)] != ref)[0]
     assert bad.size == 0, "first mismatch at byte %d of %d" % (bad[0], len(ref))
     assert (got[len(ref):] == 0xA5).all()
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("WSG_FUZZ_SEEDS", 60)) // 2))
+def test_fuzz_fanout_many_vs_oracle(codec, seed):
+    """The ws_multicast tick (wsg_fanout_encode_many): 1-40 messages whose
+    lengths and opcodes repeat (same-geometry messages share a launch of the
+    period kernel, whose shape — waves per CU per message, no cap — was
+    retuned in round 6) or differ, 1-3000 keys, mask flag, unaligned message
+    starts; every message's frames vs oracle.fanout_encode, the gaps between
+    messages and the bytes past the last frame untouched."""
+    rng = np.random.default_rng(9000 + seed)
+    m = int(rng.integers(1, 41))
+    pool = [int(rng.choice([int(rng.integers(0, 126)), int(rng.integers(126, 9000)), 4096, 4092, 4088]))
+            for _ in range(int(rng.integers(1, 4)))]
+    lens = np.array([pool[int(rng.integers(0, len(pool)))] for _ in range(m)])
+    ops = np.array([int(rng.choice([0x82, 0x81, 0x89])) for _ in range(m)])
+    k = int(rng.integers(1, 3000))
+    mask = bool(rng.random() < 0.8)
+    keys = rng.integers(0, 2**32, k, dtype=np.uint64).astype(np.uint32)
+    src = np.zeros(m, np.uint64)
+    src[1:] = np.cumsum(lens[:-1] + rng.integers(0, 17, m - 1))
+    arena = wl.random_bytes(rng, int(src[-1] + lens[-1] + 16))
+    total = 0
+    for i in range(m):
+        total = (total + 127) // 128 * 128 + k * int(ca.frame_size(int(ops[i]), mask, int(lens[i])))
+    wire = torch.full((total + 256,), 0xA5, dtype=torch.uint8, device="cuda")
+    wire_t, off = codec.fanout_many(torch.from_numpy(arena).cuda(), src, lens, ops,
+                                    torch.from_numpy(keys.view(np.int32)).cuda(), mask=mask, wire=wire)
+    codec.sync()
+    got = wire.cpu().numpy()
+    covered = np.zeros(len(got), bool)
+    for i in range(m):
+        msg = arena[int(src[i]): int(src[i]) + int(lens[i])]
+        ref = oracle.fanout_encode(msg, keys, int(ops[i]), mask)
+        a = int(off[i])
+        bad = np.nonzero(got[a: a + len(ref)] != ref)[0]
+        assert bad.size == 0, "message %d of %d: first mismatch at byte %d of %d" % (i, m, bad[0], len(ref))
+        covered[a: a + len(ref)] = True
+    assert (got[~covered] == 0xA5).all()
