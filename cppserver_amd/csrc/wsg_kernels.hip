@@ -2083,7 +2083,12 @@ __global__ __launch_bounds__(1024) void k_fanout_period(const uint8_t* __restric
     // rotations as one v_alignbit each, and a wave-uniform test for whole
     // rows, so a pass is ~2 shuffles, ~12 VALU and one 1 KiB store.
     const uint32_t sa = 8u * (pa & 3u), sbr = 8u * (pb & 3u);
-    const uint64_t full_rows_end = chunks & ~uint64_t(63);   // rows below this are whole (64 chunks)
+    // rows below this are whole: 64 chunks, each all 16 bytes inside the
+    // output (from whole chunks only: when the job's last chunk is partial
+    // and ends a row, that row takes the byte-exact store below — counted
+    // from `chunks`, its whole-chunk store wrote up to 15 bytes past the
+    // last frame; profiles/r6/fan_gap_seed123.log)
+    const uint64_t full_rows_end = (total / CHUNK) & ~uint64_t(63);
     // this wave's passes (rows row0 + it * rstep below chunks), the first
     // n_full of them whole rows: 32-bit scalar loop counters instead of
     // 64-bit row compares in the loop

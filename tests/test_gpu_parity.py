@@ -488,6 +488,62 @@ def test_fanout_many_geometries(length, k, opcode):
         c.close()
 
 
+@pytest.mark.parametrize("length,k,opcode,m", [
+    (4096, 127, 0x82, 1),    # C4's geometry (F = 4104, P = 2): 32576 chunks = 509 whole rows, the last chunk 8 bytes
+    (4096, 127, 0x82, 3),
+    (4092, 2558, 0x81, 2),   # F = 4100, P = 4: 655488 chunks (10242 rows), the last chunk 8 bytes
+    (4092, 1343, 0x82, 1),   # F = 4100: 344,138 chunks (not a whole row count), the last chunk 12 bytes
+])
+def test_fanout_last_chunk_partial_ends_a_row(length, k, opcode, m):
+    """The period kernel's last row when the job's last 16-byte chunk is
+    partial and the chunk count is a multiple of 64 (the row is otherwise
+    whole): nothing may be written past the last frame — the whole-row store
+    of round 5 wrote the next frame's first bytes there (up to 15), past the
+    caller's capacity when wire_cap is the exact size.  Found by
+    test_fuzz_fanout_many_vs_oracle (seed 123).  The output buffer is exactly
+    the frames' size with a sentinel allocation behind it, and the messages of
+    a many-message call must leave their alignment gaps untouched."""
+    rng = np.random.default_rng(k)
+    keys = rng.integers(0, 2**32, k, dtype=np.uint64).astype(np.uint32)
+    c = ca.Codec(0)
+    try:
+        for mask in (True, False):
+            fsz = frame_size(opcode, mask, length)
+            if m == 1:
+                payload = wl.random_bytes(rng, length)
+                ref = oracle.fanout_encode(payload, keys, opcode, mask)
+                assert len(ref) == fsz * k
+                buf = torch.full((len(ref) + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+                c.fanout(dev(payload), dev(keys.view(np.int32)), opcode, mask, wire=buf[: len(ref)], length=length)
+                c.sync()
+                got = buf.cpu().numpy()
+                assert np.array_equal(got[: len(ref)], ref), mask
+                assert (got[len(ref):] == 0xA5).all(), np.nonzero(got[len(ref):] != 0xA5)[0][:16]
+            else:
+                lens = np.full(m, length)
+                ops = np.full(m, opcode)
+                src = np.zeros(m, np.uint64)
+                src[1:] = np.cumsum(lens[:-1] + 5)
+                arena = wl.random_bytes(rng, int(src[-1] + lens[-1] + 16))
+                need = 0
+                for _ in range(m):
+                    need = (need + 127) // 128 * 128 + fsz * k
+                buf = torch.full((need + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+                _, off = c.fanout_many(dev(arena), src, lens, ops, dev(keys.view(np.int32)), mask=mask,
+                                       wire=buf[:need])
+                c.sync()
+                got = buf.cpu().numpy()
+                covered = np.zeros(len(got), bool)
+                for i in range(m):
+                    ref = oracle.fanout_encode(arena[int(src[i]): int(src[i]) + length], keys, opcode, mask)
+                    a = int(off[i])
+                    assert np.array_equal(got[a: a + len(ref)], ref), (i, mask)
+                    covered[a: a + len(ref)] = True
+                assert (got[~covered] == 0xA5).all(), np.nonzero((got != 0xA5) & ~covered)[0][:16]
+    finally:
+        c.close()
+
+
 def test_fanout_many_capacity(codec):
     keys = torch.zeros(4, dtype=torch.int32, device="cuda")
     with pytest.raises(ca.WSGError) as e:
