@@ -319,7 +319,10 @@ void WSReceiveBatch::Drain(WebSocket& ws)
             Release(b.out);
         }
     } free_mine{mine, DrainRecs()};
-    const uint8_t* base = Unmask(mine);
+    // (on this thread's own codec: the batch's contexts — its codec, or one per
+    // device after SetDevices — are the running flush's, and a context is
+    // one thread's at a time)
+    const uint8_t* base = Unmask(mine, true);
     DrainRecs() = &mine.recs;   // (a Forget(ws) from one of these callbacks drops the rest)
     for (size_t r = 0; r < mine.recs.size(); ++r) {
         const Rec rec = mine.recs[r];
@@ -336,7 +339,7 @@ void WSReceiveBatch::Drain(WebSocket& ws)
     }
 }
 
-const uint8_t* WSReceiveBatch::Unmask(Batch& b)
+const uint8_t* WSReceiveBatch::Unmask(Batch& b, bool thread_codec)
 {
     // No frame with a key to apply (unmasked frames, or key 0: the
     // server-to-client direction of every reference session, ws.cpp:206):
@@ -350,7 +353,11 @@ const uint8_t* WSReceiveBatch::Unmask(Batch& b)
         throw std::length_error("WSReceiveBatch: more than 2^32-1 frames in one flush");
     b.info.resize(n);
     Grow(b.out, b.wire.len);
-    if (_devs.size() > 1)
+    if (thread_codec)
+        check(wsg_decode_batch_host(ThreadCodec(), b.wire.p, b.wire.len, b.fs.data(), uint32_t(n), b.out.p,
+                                    b.info.data()),
+              "wsg_decode_batch_host");
+    else if (_devs.size() > 1)
         check(wsg_decode_batch_host_multi(_devs.data(), int(_devs.size()), b.wire.p, b.wire.len, b.fs.data(),
                                           uint32_t(n), b.out.p, b.info.data()),
               "wsg_decode_batch_host_multi");

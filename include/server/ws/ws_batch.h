@@ -186,7 +186,8 @@ public:
     //! of that flush); ws's frames still queued then are unmasked and
     //! delivered here without the others, and with no flush running the
     //! whole queue is flushed.  From inside a callback of this thread's own
-    //! flush it returns at once.
+    //! flush it returns at once.  No frame of ws may be fed meanwhile (the
+    //! connection's reads wait while it switches batches: SetReceiveBatch).
     void Drain(WebSocket& ws);
     //! Unmask every queued frame on the GPU and deliver them in arrival
     //! order; returns the number of frames delivered.  A Flush() called from
@@ -232,8 +233,9 @@ private:
 
     void Emit(WebSocket& ws, const uint8_t* frame, uint64_t total, uint32_t hdr, const uint8_t* key);
     void ApplyPending(size_t from);
-    //! the batch's GPU pass (when a frame has a key); where the payloads lie
-    const uint8_t* Unmask(Batch& b);
+    //! the batch's GPU pass (when a frame has a key); where the payloads lie.
+    //! thread_codec: on the calling thread's codec instead of the batch's
+    const uint8_t* Unmask(Batch& b, bool thread_codec = false);
     //! this thread's Drain delivery in progress (its records), or nullptr
     static std::vector<Rec>*& DrainRecs();
     static void Grow(Pinned& b, uint64_t need);

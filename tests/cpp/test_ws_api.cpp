@@ -15,6 +15,10 @@
 #include "tls_test_certs.h"
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
@@ -119,16 +123,17 @@ struct EchoSession : WSSession {
     }
 };
 
-struct Pair {
+template <class S = EchoSession>
+struct PairT {
     Loopback ct, st;
     std::shared_ptr<EchoClient> client;
-    std::shared_ptr<EchoSession> session;
-    Pair()
+    std::shared_ptr<S> session;
+    PairT()
     {
         ct.peer = &st;
         st.peer = &ct;
         client = std::make_shared<EchoClient>(ct);
-        session = std::make_shared<EchoSession>(st);
+        session = std::make_shared<S>(st);
         session->Connect();
         client->Connect();
         pump();   // upgrade request -> 101 response
@@ -150,6 +155,7 @@ struct Pair {
         }
     }
 };
+using Pair = PairT<>;
 
 static void test_echo()
 {
@@ -572,6 +578,98 @@ static void test_multicast_tick()
 
 // One explicit send batch fed from several threads at once (a WSServer's
 // sessions on different IO threads), flushed from yet another.
+// A session whose first delivery runs a hook (test_cross_thread_drain_keyed)
+struct HookSession : EchoSession {
+    using EchoSession::EchoSession;
+    std::function<void()> on_first;
+    int calls = 0;
+    void onWSReceived(const void* b, size_t n) override
+    {
+        EchoSession::onWSReceived(b, n);
+        if (calls++ == 0 && on_first)
+            on_first();
+    }
+};
+
+// Two threads flushing two receive batches, each from inside a callback
+// moving a session off the OTHER batch while its masked frame is still
+// queued there (WSReceiveBatch::Drain): the frame is unmasked on
+// the moving thread's own codec — the other batch's contexts (one batch split
+// over two contexts of the GPU) belong to its running flush — and delivered
+// before SetReceiveBatch returns, bit-exact; the flushes do not wait for
+// each other.  The host-only form of this test (unmasked frames) runs under
+// the sanitizers (tests/cpp/test_batch_threads.cpp).
+static void test_cross_thread_drain_keyed()
+{
+    setenv("WSG_HOST_MULTI_SHARE", "1", 1);
+    for (int iter = 0; iter < 20; ++iter) {
+        WSReceiveBatch x(nullptr), y(nullptr);
+        y.SetDevices({0, 0});
+        PairT<HookSession> tx, ty;   // the first delivery of each flush
+        Pair sx, sy;                 // moved off y (by x's flusher) / off x (by y's flusher)
+        for (EchoSession* s : {static_cast<EchoSession*>(tx.session.get()), static_cast<EchoSession*>(ty.session.get()),
+                               sx.session.get(), sy.session.get()})
+            s->echo = false;
+        tx.session->SetReceiveBatch(&x);
+        ty.session->SetReceiveBatch(&y);
+        sx.session->SetReceiveBatch(&y);
+        sy.session->SetReceiveBatch(&x);
+        std::mt19937 gen(1000 + iter);
+        auto frame = [&](auto& p, size_t n) {
+            std::vector<uint8_t> payload(n);
+            for (auto& b : payload)
+                b = uint8_t(gen());
+            CHECK(p.client->SendBinaryAsync(payload.data(), payload.size()));   // masked with the client's key
+            return payload;
+        };
+        const auto ptx = frame(tx, 700), pty = frame(ty, 3000), psx = frame(sx, 40 + iter), psy = frame(sy, 5000);
+        std::mutex m;
+        std::condition_variable cv;
+        int inside = 0;
+        std::atomic<int> done{0};
+        auto both_inside = [&] {
+            std::unique_lock<std::mutex> g(m);
+            ++inside;
+            cv.notify_all();
+            cv.wait(g, [&] { return inside == 2; });
+        };
+        auto move_off = [&](Pair& p, const std::vector<uint8_t>& want) {
+            std::vector<uint8_t> b(p.st.inbox.begin(), p.st.inbox.end());
+            p.st.inbox.clear();
+            p.session->onReceived(b.data(), b.size());   // queued in the batch the other thread flushes
+            p.session->SetReceiveBatch(nullptr);         // delivered before this returns
+            CHECK(p.session->last == want);
+        };
+        tx.session->on_first = [&] { both_inside(); move_off(sx, psx); };
+        ty.session->on_first = [&] { both_inside(); move_off(sy, psy); };
+        auto feed = [](auto& p) {
+            std::vector<uint8_t> b(p.st.inbox.begin(), p.st.inbox.end());
+            p.st.inbox.clear();
+            p.session->onReceived(b.data(), b.size());
+        };
+        feed(tx);
+        feed(ty);
+        std::thread watchdog([&] {
+            for (int i = 0; i < 300 && done.load() < 2; ++i)
+                std::this_thread::sleep_for(std::chrono::milliseconds(100));
+            if (done.load() < 2) {
+                std::fprintf(stderr, "cross-thread drain (keyed): flushes blocked on each other\n");
+                std::_Exit(3);
+            }
+        });
+        std::thread a([&] { x.Flush(); ++done; });
+        std::thread b([&] { y.Flush(); ++done; });
+        a.join();
+        b.join();
+        watchdog.join();
+        CHECK(tx.session->last == ptx && ty.session->last == pty);
+        CHECK(x.Flush() == 0 && y.Flush() == 0);   // nothing left behind
+        tx.session->SetReceiveBatch(nullptr);
+        ty.session->SetReceiveBatch(nullptr);
+    }
+    unsetenv("WSG_HOST_MULTI_SHARE");
+}
+
 static void test_batch_threads()
 {
     WSSendBatch batch;
@@ -803,6 +901,7 @@ int main()
         test_auto_batch_echo();
         test_multicast_tick();
         test_batch_threads();
+        test_cross_thread_drain_keyed();
         test_wss();
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());
