@@ -178,3 +178,58 @@ def test_fuzz_fanout_many_vs_oracle(codec, seed):
         assert bad.size == 0, "message %d of %d: first mismatch at byte %d of %d" % (i, m, bad[0], len(ref))
         covered[a: a + len(ref)] = True
     assert (got[~covered] == 0xA5).all()
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("WSG_FUZZ_SEEDS", 150)) // 3))
+def test_fuzz_nothing_written_past_the_output(codec, seed):
+    """Outputs of exactly the size the contract gives (encode: the frames'
+    bytes as wire_cap; decode: wire_len bytes of output, out of place and in
+    place), each inside a larger buffer filled with a sentinel: the frames
+    equal the oracle's and not one byte past the output changes — through
+    the device entry points and both host paths (page-locked buffers: the
+    lane for small batches, the launch path for larger ones).  A whole
+    16-byte store of a partial last chunk would write up to 15 bytes past
+    a caller's buffer; the fan-out's period kernel did that (round 6)."""
+    payload, desc = _batch(1000 + seed)
+    wire_o, off_o = oracle.encode_batch(payload, desc)
+    n, total = len(desc), len(wire_o)
+    S = 0xA5
+    # device encode into wire_cap == total
+    p = torch.from_numpy(payload if len(payload) else np.zeros(1, np.uint8)).cuda()
+    d = ca.desc_to_tensor(desc, "cuda")
+    buf = torch.full((total + 64,), S, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(p, d, wire=buf[: max(total, 1)], wire_cap=total)
+    assert codec.sync_status() == 0
+    got = buf.cpu().numpy()
+    assert np.array_equal(got[:total], wire_o)
+    assert (got[total:] == S).all(), np.nonzero(got[total:] != S)[0][:8]
+    fs = off_o[:-1].copy()
+    rc_o, out_o, _ = oracle.decode_batch(wire_o, fs)
+    f = torch.from_numpy(fs.view(np.int64)).cuda()
+    # device decode: out of place, then in place, wire_len == total
+    src = torch.from_numpy(wire_o if total else np.zeros(1, np.uint8)).cuda()[:total]
+    obuf = torch.full((total + 64,), S, dtype=torch.uint8, device="cuda")
+    codec.decode_batch(src, f, out=obuf[:total])
+    assert codec.sync_status() == rc_o
+    got = obuf.cpu().numpy()
+    assert np.array_equal(got[:total], out_o) and (got[total:] == S).all()
+    ibuf = torch.full((total + 64,), S, dtype=torch.uint8, device="cuda")
+    ibuf[:total] = src
+    codec.decode_batch(ibuf[:total], f, out=ibuf[:total])
+    assert codec.sync_status() == rc_o
+    got = ibuf.cpu().numpy()
+    assert np.array_equal(got[:total], out_o) and (got[total:] == S).all()
+    # host paths, page-locked buffers with the sentinel behind the output
+    pin_p = ca.pinned_empty(max(len(payload), 1))
+    pin_p[: len(payload)] = payload
+    pin_w = ca.pinned_empty(total + 64)
+    pin_w[:] = S
+    rc, wire_h, off_h = codec.encode_batch_host(pin_p[: len(payload)], desc, wire=pin_w[:total])
+    assert rc == 0 and np.array_equal(pin_w[:total], wire_o) and (pin_w[total:] == S).all()
+    pin_in = ca.pinned_empty(max(total, 1))
+    pin_in[:total] = wire_o
+    pin_out = ca.pinned_empty(total + 64)
+    pin_out[:] = S
+    rc, out_h, _ = codec.decode_batch_host(pin_in[:total], fs, out=pin_out[:total])
+    assert rc == rc_o and np.array_equal(pin_out[:total], out_o) and (pin_out[total:] == S).all()
+    assert n == len(fs)
