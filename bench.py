@@ -1181,25 +1181,6 @@ def fanout_many_leg(w, m=16, reps=10):
                                   "what": "zero_() of the same bytes, back to back (the runtime's fill)"}}
 
 
-def c4_per_launch(w, launches=200):
-    """One C4 fan-out at a time with HIP events around each launch on its
-    stream (the library's timing hook): the kernel's own duration, as a
-    kernel trace measures it, and its frac; the line's roofline keeps the
-    region's (conservative) average."""
-    c = w.codec
-    c.timing(True, every=1)
-    c.timing_read(reset=True)
-    for _ in range(launches):
-        w.step()
-    lo, hi = c.timing_minmax()
-    ms, n = c.timing_read(reset=True)
-    c.timing(False)
-    avg = ms / max(n, 1)
-    return {"launches": n, "avg_us": round(avg * 1e3, 3), "min_us": round(lo * 1e3, 3), "max_us": round(hi * 1e3, 3),
-            "achieved_GBps": round(w.alg_bytes / (avg * 1e-3) / 1e9, 1),
-            "frac": round(w.alg_bytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
-
-
 def c4_graph_leg(w, steps, reps=5):
     """C4 as a captured graph of `steps` fan-out launches, replayed `reps`
     times; HIP events around each replay.  Per-launch time and its frac."""
@@ -1408,10 +1389,6 @@ def config_obj(args, cfg, codec, rank, world, device, steps, warmup, cpu):
             # and replayed once (a Python call per launch costs ~6-7 us, close
             # to the 8 us kernel, and can bound the eager region on a slow host)
             obj["graph_replay"] = c4_graph_leg(w, steps)
-            # the kernel alone: HIP events around every launch (the region's
-            # events above also hold the ~0.4 us between dependent launches,
-            # which a rocprofv3 trace's per-kernel durations do not)
-            obj["per_launch_events"] = c4_per_launch(w)
             # the ws_multicast tick's form: 16 such messages in ONE launch
             # (wsg_fanout_encode_many), where one 41 MB fan-out is too short
             # to reach the write rate on its own
