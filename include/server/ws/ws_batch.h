@@ -15,7 +15,8 @@
  * every connection sees exactly the onWS* calls PrepareReceiveFrame would
  * have made, only later.
  *
- * Callback buffers are valid until the next Flush().  Feed / Clear / Forget
+ * Callback buffers are valid until the next Flush() (those of a Drain's own
+ * delivery until it returns).  Feed / Clear / Forget
  * may come from any thread (a mutex guards the queue, as the reference's
  * per-session strands and locks let any IO thread call in); a Flush runs on
  * the calling thread with that thread's GPU codec context unless the batch
