@@ -152,6 +152,10 @@ def dist_setup(args):
             os.environ.setdefault("NCCL_HOSTID", "wsg-bench-rank-%d" % rank)
             os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
             os.environ.setdefault("NCCL_IB_DISABLE", "1")
+        # one node (the driver's launch): RCCL's bootstrap over loopback, as
+        # the rendezvous itself (127.0.0.1); the data path between the GPUs is
+        # RCCL's P2P over xGMI either way
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         torch.cuda.set_device(local)
         # The bench's own group is gloo: barriers, max over ranks and the
         # product's RCCL id travel over host sockets, so the only RCCL in a
