@@ -1409,13 +1409,14 @@ def config_obj(args, cfg, codec, rank, world, device, steps, warmup, cpu):
         w.close()
 
 
-def decode_launches(w, launches=60, warm=10):
+def decode_launches(w, launches=60, warm=30):
     """C3's decode half launch by launch: k_decode alone
     on the round trip's wire, HIP events between launches (one launch per
     decode_batch call), after the timed region, behind `warm` untimed
     launches of its own (the synchronize before it idles the GPU, and the
-    first launches after an idle GPU run slow: 0.72-0.80 ms against 0.66-0.69
-    in round 5's first_5_ms)."""
+    first ~15 ms of load after an idle GPU run slow: with 10 warm launches,
+    7 ms, round 5's first_5_ms were 0.72-0.74 ms against a 0.676 median;
+    30 cover the ramp)."""
     import statistics
 
     t = w.torch
