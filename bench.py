@@ -765,7 +765,8 @@ def echo_c1_leg(seconds=3.0, timeout=120):
             if len(runs) > 1:
                 tr[leg]["runs_msg_per_s"] = [x["msg_per_s"] for x in runs]
             if a[0] != "cpu_ref":   # socket reads, lane requests and launches of the reported run
-                tr[leg]["lane"] = {k: d.get(k) for k in ("reads", "lane_requests", "lane_launches", "lane_state")}
+                tr[leg]["lane"] = {k: d.get(k) for k in ("reads", "lane_requests", "lane_launches", "lane_state",
+                                                           "lane_give_ups")}
         tr["what"] = ("ws_echo over TCP 127.0.0.1 (one process, server and client on their own epoll threads): "
                       "gpu = the drop-in WSClient/WSSession, cpu_ref = the oracle's restatement of the reference "
                       "codec (no GPU); 100-client legs: median of 3 runs (runs_msg_per_s); the published figures below are "

@@ -218,7 +218,7 @@ double seconds(Clock::time_point a, Clock::time_point b) { return std::chrono::d
 // One IO thread: its connections' ends (client ends or server ends), one epoll set.
 // Per-run path counters: socket reads, and this process's lane use as the
 // IO threads' codec contexts saw it (wsg_lane_stats at each thread's end).
-std::atomic<uint64_t> g_reads{0}, g_lane_requests{0}, g_lane_launches{0};
+std::atomic<uint64_t> g_reads{0}, g_lane_requests{0}, g_lane_launches{0}, g_lane_give_ups{0};
 std::atomic<int> g_lane_state{2};   // lowest seen: -1 given up, 0 not running, 1 running (2: none read)
 
 void io_loop(std::vector<End*>& ends, bool tick, double secs, bool client_side, std::atomic<int>& done_clients,
@@ -292,6 +292,12 @@ void io_loop(std::vector<End*>& ends, bool tick, double secs, bool client_side, 
             }
             int cur = g_lane_state.load();
             while (st < cur && !g_lane_state.compare_exchange_weak(cur, st)) {
+            }
+        }
+        uint64_t gu = 0;
+        if (wsg_lane_events(ThreadCodec(), &gu, nullptr) == WSG_OK) {   // (the device's lane: the same for all)
+            uint64_t m = g_lane_give_ups.load();
+            while (gu > m && !g_lane_give_ups.compare_exchange_weak(m, gu)) {
             }
         }
     }
@@ -407,11 +413,12 @@ int main(int argc, char** argv)
         std::printf("{\"codec\": \"%s\", \"transport\": \"TCP 127.0.0.1 (epoll)\", \"clients\": %d, \"threads\": %d, "
                     "\"messages_in_flight\": %zu, \"size\": %zu, \"seconds\": %.3f, \"total_messages\": %llu, "
                     "\"msg_per_s\": %.0f, \"MiB_per_s\": %.3f, \"latency_ns\": %.1f, \"payload_ok\": %s, \"reads\": %llu, "
-                    "\"lane_requests\": %llu, \"lane_launches\": %llu, \"lane_state\": %d}\n",
+                    "\"lane_requests\": %llu, \"lane_launches\": %llu, \"lane_state\": %d, \"lane_give_ups\": %llu}\n",
                     codec.c_str(), clients, threads, messages, size, el, (unsigned long long)msgs, msgs / el,
                     total / el / (1 << 20), msgs ? el * 1e9 / double(msgs) : 0.0, bad == 0 ? "true" : "false",
                     (unsigned long long)g_reads.load(), (unsigned long long)g_lane_requests.load(),
-                    (unsigned long long)g_lane_launches.load(), g_lane_state.load());
+                    (unsigned long long)g_lane_launches.load(), g_lane_state.load(),
+                    (unsigned long long)g_lane_give_ups.load());
     } catch (const std::exception& e) {
         std::fprintf(stderr, "bench_echo_tcp: %s\n", e.what());
         return 3;
